@@ -1,0 +1,171 @@
+"""Throughput benchmark of the MI355X DBSR forward (BASELINE.json metric: bursts/s on
+SyntheticBurstVal-shaped 14x48x48 RAW bursts -> 384x384 RGB, configs[1]: bf16, batch 8 per GPU).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 8] [--frames 14] [--size 48]
+                  [--dtype bf16|fp32] [--no-graph] [--no-cpu-baseline]
+
+One process per GPU (torchrun for N>1); every rank runs its own batch of independent bursts (the
+path shards over bursts with no data-path collective: weak scaling).  A step = one full forward
+(PWC-Net alignment, encoder, warp, merging/fusion incl. the fusion_weights aux output, decoder) over
+one batch of synthetic bursts already resident in HBM, replayed as one HIP graph.  Timing: W untimed
+steps, then K steps bracketed by barrier + synchronize, max over ranks.  Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+PEAK_MFMA_TFLOPS = {'bf16': 2500.0, 'fp32': 157.3}    # dense peaks (MI355X_MICROARCH.md chip table)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=5)
+    ap.add_argument('--batch', type=int, default=8)
+    ap.add_argument('--frames', type=int, default=14)
+    ap.add_argument('--size', type=int, default=48)
+    ap.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
+    ap.add_argument('--no-graph', action='store_true')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-seconds', type=float, default=15.0)
+    ap.add_argument('--kernel-breakdown', action='store_true', help='print per-op device times to stderr')
+    return ap.parse_args()
+
+
+def cpu_baseline(N, H, W, seconds):
+    """Oracle (torch-CPU restatement of the reference forward, oracle/dbsr_oracle.py) timed on this
+    node's host cores on a bounded sample: batch-1 bursts of the same workload, fp32, until
+    `seconds` of CPU work have elapsed."""
+    from oracle import dbsr_oracle as orc
+    import dbsr_amd
+    from dbsr_amd import arch
+    from dbsr_amd.weights import generate_state_dict
+    from dbsr_amd.burst import synthetic_bursts
+    net = dbsr_amd.dbsrnet_cvpr2021(**dbsr_amd.DBSR_SYNTHETIC_KWARGS)
+    sd = orc.state_dict_to_torch(generate_state_dict(arch.state_dict_shapes(net), seed=0))
+    burst, _ = synthetic_bursts(1, N, H, W, sr_factor=8, seed=1)
+    with torch.no_grad():
+        orc.dbsr_forward(burst, sd)              # warm-up
+        n, t0 = 0, time.perf_counter()
+        while True:
+            orc.dbsr_forward(burst, sd)
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= seconds or n >= 50:
+                break
+    return {'value': n / el, 'unit': 'bursts/s', 'cores': torch.get_num_threads(), 'kind': 'port',
+            'sample': f'{n} batch-1 bursts of {N}x{H}x{W} (fp32 oracle/dbsr_oracle.py, {el:.1f} s)'}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    dist = world > 1
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+    if dist:
+        import torch.distributed as td
+        td.init_process_group('nccl', device_id=dev)
+
+    import dbsr_amd
+    from dbsr_amd.burst import synthetic_bursts
+    dtype = torch.bfloat16 if args.dtype == 'bf16' else torch.float32
+    net = dbsr_amd.build_synthetic_net(seed=0).to(dev).eval()
+    net.set_compute_dtype(dtype)
+    net.use_graph = not args.no_graph
+    B, N, S = args.batch, args.frames, args.size
+    burst, _ = synthetic_bursts(B, N, S, S, sr_factor=8, seed=1000 + rank)
+    burst = burst.to(dev)
+
+    with torch.no_grad():
+        for _ in range(max(1, args.warmup)):
+            net(burst)
+        torch.cuda.synchronize()
+        if dist:
+            td.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            net(burst)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        if dist:
+            t = torch.tensor([el], device=dev)
+            td.all_reduce(t, op=td.ReduceOp.MAX)
+            el = float(t.item())
+            td.barrier()
+
+        # ---- per-kernel device times (HIP events on the plan's stream), outside the timed region ----
+        eng = net._engine
+        plan = eng.plans[(B, N, S, S)]
+        times = plan.time_ops(torch.cuda.current_stream(dev).cuda_stream, reps=10)
+
+    ms_step = el / args.steps * 1e3
+    value = world * B * args.steps / el
+    fam = {}
+    for i, (name, ms) in enumerate(times):
+        kind = 'conv' if i in plan.work and plan.work[i][0] == 'flop' else name.split('.')[-1]
+        f = fam.setdefault(kind, [0.0, 0.0, 0])
+        f[0] += ms
+        f[1] += plan.work[i][1] if i in plan.work else 0.0
+        f[2] += 1
+    conv_ms, conv_flop, _ = fam['conv']
+    peak_t = PEAK_MFMA_TFLOPS[args.dtype]
+    conv_tf = conv_flop / (conv_ms * 1e-3) / 1e12
+    roof = {'bound': 'mfma', 'kernel': 'conv2d_kernel (all %d conv launches of one forward)' % fam['conv'][2],
+            'achieved': round(conv_tf, 2), 'peak': peak_t, 'unit': 'TFLOP/s', 'frac': round(conv_tf / peak_t, 4),
+            'traffic': None}
+    hbm = {}
+    for k in ('warp', 'fuse'):
+        if k in fam:
+            ms, by, _ = fam[k]
+            gbs = by / (ms * 1e-3) / 1e9
+            hbm[k] = {'bound': 'hbm', 'achieved': round(gbs, 1), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
+                      'frac': round(gbs / PEAK_HBM_GBS, 4), 'traffic': None, 'us': round(ms * 1e3, 2),
+                      'alg_bytes': by}
+    if args.kernel_breakdown and rank == 0:
+        for name, ms in times:
+            print(f'{name:32s} {ms * 1e3:9.1f} us', file=sys.stderr)
+        for k, (ms, w, n) in sorted(fam.items(), key=lambda kv: -kv[1][0]):
+            print(f'[family] {k:12s} {ms * 1e3:9.1f} us  n={n}', file=sys.stderr)
+        print(f'sum of op times {sum(t for _, t in times) * 1e3:.1f} us vs step {ms_step * 1e3:.1f} us',
+              file=sys.stderr)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(N, S, S, args.cpu_seconds)
+
+    if rank == 0:
+        out = {
+            'metric': 'bursts/sec 14x48x48 RAW->4x (SyntheticBurstVal shape), DBSR forward',
+            'value': round(value, 2), 'unit': 'bursts/s', 'n_gpus': world, 'steps': args.steps,
+            'warmup': args.warmup, 'ms_per_step': round(ms_step, 4), 'higher_is_better': True, 'scaling': 'weak',
+            'vs_baseline': None, 'dtype': args.dtype, 'data': 'synthetic (seeded bursts, seeded random weights)',
+            'config': {'workload': 'configs[1]: SyntheticBurstVal 14-frame 48x48 -> 384x384 (sr x8 of RAW, x4 of '
+                                   'full-res), batch %d per GPU, full PWC-Net + warp + fusion + decoder' % B,
+                       'global_batch': B * world, 'frames': N, 'height': S, 'width': S, 'out_size': S * 8,
+                       'parallelism': 'dp%d (independent bursts per rank)' % world,
+                       'hip_graph': not args.no_graph, 'fusion_weights_written': True},
+            'roofline': roof, 'roofline_hbm': hbm,
+            'cpu_baseline': cpu,
+            'conv_flop_per_step': conv_flop,
+        }
+        print(json.dumps(out))
+    if dist:
+        td.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,128 @@
+"""ctypes binding of libdbsr_hip.so (C ABI: include/dbsr_hip.h).
+
+torch is imported first so that the library's libamdhip64.so.7 dependency resolves to the HIP
+runtime torch already loaded (same SONAME) and kernels share torch's streams and allocations.
+There is no fallback: if the library is missing or fails to load, every op raises.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get('DBSR_HIP_LIB', os.path.join(_HERE, 'libdbsr_hip.so'))
+
+DBSR_F32, DBSR_BF16 = 0, 1
+ACT_NONE, ACT_RELU, ACT_LRELU = 0, 1, 2
+OUT_NHWC, OUT_SHUFFLE, OUT_NCHW_F32 = 0, 1, 2
+ABI_VERSION = 1
+
+
+class FrameMap(ctypes.Structure):
+    _fields_ = [('fpg', ctypes.c_int), ('group_stride', ctypes.c_int), ('group_offset', ctypes.c_int),
+                ('inner_stride', ctypes.c_int)]
+
+
+IDENTITY = (1, 1, 0, 1)
+
+
+class Tensor(ctypes.Structure):
+    _fields_ = [('ptr', ctypes.c_void_p), ('dtype', ctypes.c_int), ('img_stride', ctypes.c_longlong),
+                ('ld', ctypes.c_int), ('c0', ctypes.c_int), ('map', FrameMap)]
+
+
+class ConvDesc(ctypes.Structure):
+    _fields_ = [('n_frames', ctypes.c_int),
+                ('x', Tensor), ('in_h', ctypes.c_int), ('in_w', ctypes.c_int), ('cin', ctypes.c_int),
+                ('w', ctypes.c_void_p), ('bias', ctypes.c_void_p), ('cout', ctypes.c_int), ('kh', ctypes.c_int),
+                ('kw', ctypes.c_int), ('stride', ctypes.c_int), ('pad', ctypes.c_int), ('dil', ctypes.c_int),
+                ('y', Tensor), ('out_h', ctypes.c_int), ('out_w', ctypes.c_int),
+                ('act', ctypes.c_int),
+                ('res', Tensor), ('post_act', ctypes.c_int),
+                ('out_mode', ctypes.c_int), ('shuffle', ctypes.c_int)]
+
+
+_lib = None
+
+
+class DBSRLibError(RuntimeError):
+    pass
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise DBSRLibError('libdbsr_hip.so not found at %s: build it with `make` (or __graft_entry__.build())'
+                               % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        c_int, c_void_p, c_float, c_ll, c_size_t = (ctypes.c_int, ctypes.c_void_p, ctypes.c_float,
+                                                    ctypes.c_longlong, ctypes.c_size_t)
+        sigs = {
+            'dbsr_abi_version': ([], c_int),
+            'dbsr_last_error': ([], ctypes.c_char_p),
+            'dbsr_conv_packed_elems': ([c_int, c_int, c_int, c_int], c_size_t),
+            'dbsr_conv_pack_weights': ([c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
+                                        c_void_p, c_void_p], c_int),
+            'dbsr_conv2d': ([ctypes.POINTER(ConvDesc), c_void_p], c_int),
+            'dbsr_correlation': ([c_int, c_int, c_int, c_int, Tensor, Tensor, Tensor, c_int, c_void_p], c_int),
+            'dbsr_backwarp': ([c_int, c_int, c_int, c_int, Tensor, Tensor, c_float, Tensor, c_void_p], c_int),
+            'dbsr_warp_bilinear': ([c_int, c_int, c_int, c_int, Tensor, c_void_p, c_ll, Tensor, c_void_p], c_int),
+            'dbsr_fuse_softmax': ([c_int, c_int, c_int, c_int, Tensor, Tensor, Tensor, Tensor, Tensor, c_void_p],
+                                  c_int),
+            'dbsr_conv_transpose_k4s2': ([c_int, c_int, c_int, c_int, c_int, Tensor, c_void_p, c_void_p, Tensor,
+                                          c_void_p], c_int),
+            'dbsr_pack_burst': ([c_int, c_int, c_int, c_int, c_void_p, Tensor, c_int, c_int, Tensor, c_void_p], c_int),
+            'dbsr_flow_finalize': ([c_int, c_int, c_int, c_int, Tensor, c_int, c_int, c_int, c_int, c_void_p, c_float,
+                                    Tensor, c_void_p], c_int),
+            'dbsr_gauss_blur3': ([c_int, c_int, c_int, c_int, Tensor, c_void_p, Tensor, c_void_p], c_int),
+            'dbsr_merge_prep': ([c_int, c_int, c_int, c_int, Tensor, Tensor, c_void_p], c_int),
+            'dbsr_pwc_assemble': ([c_int, c_int, c_int, c_int, Tensor, Tensor, Tensor, Tensor, c_void_p], c_int),
+            'dbsr_zero': ([c_void_p, c_size_t, c_void_p], c_int),
+        }
+        for name, (args, res) in sigs.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = res
+        if L.dbsr_abi_version() != ABI_VERSION:
+            raise DBSRLibError('libdbsr_hip.so ABI %d != expected %d' % (L.dbsr_abi_version(), ABI_VERSION))
+        _lib = L
+    return _lib
+
+
+EXPORTED = ['dbsr_abi_version', 'dbsr_last_error', 'dbsr_conv_packed_elems', 'dbsr_conv_pack_weights', 'dbsr_conv2d',
+            'dbsr_correlation', 'dbsr_backwarp', 'dbsr_warp_bilinear', 'dbsr_fuse_softmax',
+            'dbsr_conv_transpose_k4s2', 'dbsr_pack_burst', 'dbsr_flow_finalize', 'dbsr_gauss_blur3',
+            'dbsr_merge_prep', 'dbsr_pwc_assemble', 'dbsr_zero']
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = lib().dbsr_last_error().decode(errors='replace')
+        raise DBSRLibError('%s failed (rc=%d): %s' % (what, rc, msg))
+
+
+def dtype_code(dt):
+    if dt == torch.float32:
+        return DBSR_F32
+    if dt == torch.bfloat16:
+        return DBSR_BF16
+    raise ValueError('unsupported dtype %s' % dt)
+
+
+def tensor_desc(t, ld, c0=0, img_stride=None, fmap=IDENTITY, dtype=None):
+    """Describe a channel slice [c0, ...) of NHWC images stored in torch tensor `t` (any shape whose
+    memory is [images][pixels][ld])."""
+    if t is None:
+        return Tensor(None, 0, 0, 0, 0, FrameMap(1, 1, 0, 1))
+    if img_stride is None:
+        img_stride = t[0].numel() if t.dim() > 1 else t.numel()
+    return Tensor(t.data_ptr(), dtype_code(t.dtype if dtype is None else dtype), int(img_stride), int(ld), int(c0),
+                  FrameMap(*fmap))
+
+
+NULL_TENSOR = Tensor(None, 0, 0, 0, 0, FrameMap(1, 1, 0, 1))
+
+
+def stream_ptr(device=None):
+    return torch.cuda.current_stream(device).cuda_stream

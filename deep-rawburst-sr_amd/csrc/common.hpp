@@ -1,0 +1,91 @@
+// Shared device helpers for the gfx950 DBSR kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/dbsr_hip.h"
+
+namespace dbsr {
+
+typedef uint16_t bf16_t;                                            // storage type
+typedef __attribute__((ext_vector_type(8))) short bf16x8_t;        // MFMA bf16 operand (8 elems)
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;          // 16x16 MFMA accumulator
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
+
+__device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((unsigned)v) << 16); }
+
+// round-to-nearest-even; NaN kept NaN (MI355X_MICROARCH.md correctness table: plain cast path)
+__device__ __forceinline__ bf16_t f2bf(float f) {
+    unsigned u = __float_as_uint(f);
+    if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) return (bf16_t)((u >> 16) | 0x40);
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (bf16_t)(u >> 16);
+}
+
+template <typename T> struct elem;
+template <> struct elem<float> {
+    static __device__ __forceinline__ float ld(const float* p) { return *p; }
+    static __device__ __forceinline__ void st(float* p, float v) { *p = v; }
+};
+template <> struct elem<bf16_t> {
+    static __device__ __forceinline__ float ld(const bf16_t* p) { return bf2f(*p); }
+    static __device__ __forceinline__ void st(bf16_t* p, float v) { *p = f2bf(v); }
+};
+
+// load 8 consecutive elements as fp32
+__device__ __forceinline__ void load8(const float* p, float (&v)[8]) {
+    float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ void load8(const bf16_t* p, float (&v)[8]) {
+    u32x4_t q = *(const u32x4_t*)p;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        v[2 * i] = __uint_as_float(q[i] << 16);
+        v[2 * i + 1] = __uint_as_float(q[i] & 0xffff0000u);
+    }
+}
+__device__ __forceinline__ void store8(float* p, const float (&v)[8]) {
+    *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
+    *(float4*)(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+__device__ __forceinline__ void store8(bf16_t* p, const float (&v)[8]) {
+    u32x4_t q;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q[i] = (unsigned)f2bf(v[2 * i]) | ((unsigned)f2bf(v[2 * i + 1]) << 16);
+    *(u32x4_t*)p = q;
+}
+
+__device__ __forceinline__ long long map_frame(const dbsr_frame_map& m, int f) {
+    return (long long)(f / m.fpg) * m.group_stride + m.group_offset + (long long)(f % m.fpg) * m.inner_stride;
+}
+
+template <typename T>
+__device__ __forceinline__ T* img_ptr(const dbsr_tensor& t, int f) {
+    return (T*)t.ptr + map_frame(t.map, f) * t.img_stride + t.c0;
+}
+
+__device__ __forceinline__ float apply_act(float v, int act) {
+    if (act == DBSR_ACT_RELU) return v > 0.f ? v : 0.f;
+    if (act == DBSR_ACT_LRELU) return v > 0.f ? v : 0.1f * v;
+    return v;
+}
+
+}  // namespace dbsr
+
+// ---------------- host-side helpers ----------------
+void dbsr_set_error(const char* fmt, ...);
+#define DBSR_CHECK_ARG(cond, ...)                 \
+    do {                                          \
+        if (!(cond)) {                            \
+            dbsr_set_error(__VA_ARGS__);          \
+            return DBSR_E_ARG;                    \
+        }                                         \
+    } while (0)
+#define DBSR_LAUNCH_CHECK()                                               \
+    do {                                                                  \
+        hipError_t e_ = hipGetLastError();                                \
+        if (e_ != hipSuccess) {                                           \
+            dbsr_set_error("HIP launch error: %s", hipGetErrorString(e_)); \
+            return (int)e_;                                               \
+        }                                                                 \
+    } while (0)

@@ -1,0 +1,277 @@
+// DBSR merge-path kernels: flow-guided warp of the frame embeddings (HBM-bound), softmax-over-burst
+// fusion (HBM-bound), merge input prep and the decoder's Gaussian blur.  NHWC activations.
+#include "common.hpp"
+
+using namespace dbsr;
+
+namespace {
+
+// ------------------------------------------------------------------------------------------------
+// warp (models/layers/warp.py:19-46): sample feat at grid = (x + 0.5 + fx, y + 0.5 + fy) normalised by
+// 2g/W - 1 and unnormalised by grid_sample(align_corners=False): ((g+1)*W - 1)/2, i.e. x + fx; the
+// float op sequence of the reference is kept so sample positions round identically.
+// Thread = (pixel, 8-channel group): a wave covers 512 contiguous channels (1 KiB bf16) per tap.
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void warp_kernel(int n, int h, int w, int groups, dbsr_tensor feat,
+                                                   const float* __restrict__ flow, long long fis, dbsr_tensor out) {
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long long)n * h * w * groups) return;
+    const int g = (int)(idx % groups);
+    const long long pix = idx / groups;
+    const int hw = h * w;
+    const int p = (int)(pix / hw), rr = (int)(pix - (long long)p * hw);
+    const int y = rr / w, x = rr - y * w;
+    const float* fl = flow + (long long)p * fis + rr;
+    const float gx = ((float)x + 0.5f) + fl[0];
+    const float gy = ((float)y + 0.5f) + fl[hw];
+    const float gxn = 2.0f * gx / (float)w - 1.0f, gyn = 2.0f * gy / (float)h - 1.0f;
+    const float ix = ((gxn + 1.f) * (float)w - 1.f) / 2.f;
+    const float iy = ((gyn + 1.f) * (float)h - 1.f) / 2.f;
+    const float fx0 = floorf(ix), fy0 = floorf(iy);
+    const int x0 = (int)fx0, y0 = (int)fy0;
+    const float wx1 = ix - fx0, wx0 = 1.f - wx1, wy1 = iy - fy0, wy0 = 1.f - wy1;
+    const T* base = img_ptr<T>(feat, p) + g * 8;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const int xx = x0 + (t & 1), yy = y0 + (t >> 1);
+        const float wt = ((t & 1) ? wx1 : wx0) * ((t >> 1) ? wy1 : wy0);
+        if ((unsigned)xx < (unsigned)w && (unsigned)yy < (unsigned)h) {
+            float v[8];
+            load8(base + ((long long)yy * w + xx) * feat.ld, v);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[j] = fmaf(wt, v[j], acc[j]);
+        }
+    }
+    store8(img_ptr<T>(out, p) + (long long)rr * out.ld + g * 8, acc);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Fusion (merging.py:116-126): w = softmax_n(logits[b,n]), fused[b] = sum_n feat[b,n] * w[b,n].
+// Thread = (b, pixel, 4 channels); the N logits stay in registers (one read of each byte), fp32
+// softmax, optional write of the normalised weights (the reference's aux 'fusion_weights').
+// ------------------------------------------------------------------------------------------------
+template <typename T> struct Vec4;
+template <> struct Vec4<float> {
+    static __device__ __forceinline__ void ld(const float* p, float (&v)[4]) {
+        float4 q = *(const float4*)p;
+        v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+    }
+    static __device__ __forceinline__ void st(float* p, const float (&v)[4]) {
+        *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
+    }
+};
+template <> struct Vec4<bf16_t> {
+    static __device__ __forceinline__ void ld(const bf16_t* p, float (&v)[4]) {
+        uint2 q = *(const uint2*)p;
+        v[0] = __uint_as_float(q.x << 16); v[1] = __uint_as_float(q.x & 0xffff0000u);
+        v[2] = __uint_as_float(q.y << 16); v[3] = __uint_as_float(q.y & 0xffff0000u);
+    }
+    static __device__ __forceinline__ void st(bf16_t* p, const float (&v)[4]) {
+        uint2 q;
+        q.x = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
+        q.y = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
+        *(uint2*)p = q;
+    }
+};
+
+template <typename T, int NMAX>
+__global__ __launch_bounds__(256) void fuse_softmax_kernel(int B, int N, int hw, int groups, dbsr_tensor logits,
+                                                           dbsr_tensor ref, dbsr_tensor oth, dbsr_tensor fused,
+                                                           dbsr_tensor weights) {
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long long)B * hw * groups) return;
+    const int g = (int)(idx % groups);
+    const long long pix = idx / groups;
+    const int b = (int)(pix / hw), rr = (int)(pix - (long long)b * hw);
+    const int c = g * 4;
+    float l[NMAX][4];
+    float m[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+    for (int n = 0; n < NMAX; ++n) {
+        if (n < N) {
+            Vec4<T>::ld(img_ptr<T>(logits, b * N + n) + (long long)rr * logits.ld + c, l[n]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) m[j] = fmaxf(m[j], l[n][j]);
+        }
+    }
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int n = 0; n < NMAX; ++n) {
+        if (n < N) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                l[n][j] = __expf(l[n][j] - m[j]);
+                s[j] += l[n][j];
+            }
+        }
+    }
+    float inv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) inv[j] = 1.0f / s[j];
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int n = 0; n < NMAX; ++n) {
+        if (n < N) {
+            const T* fp = n == 0 ? img_ptr<T>(ref, b) : img_ptr<T>(oth, b * (N - 1) + n - 1);
+            const int ldf = n == 0 ? ref.ld : oth.ld;
+            float f[4], wn[4];
+            Vec4<T>::ld(fp + (long long)rr * ldf + c, f);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                wn[j] = l[n][j] * inv[j];
+                acc[j] = fmaf(f[j], wn[j], acc[j]);
+            }
+            if (weights.ptr) {
+                if (weights.dtype == DBSR_F32)
+                    Vec4<float>::st(img_ptr<float>(weights, b * N + n) + (long long)rr * weights.ld + c, wn);
+                else
+                    Vec4<bf16_t>::st(img_ptr<bf16_t>(weights, b * N + n) + (long long)rr * weights.ld + c, wn);
+            }
+        }
+    }
+    Vec4<T>::st(img_ptr<T>(fused, b) + (long long)rr * fused.ld + c, acc);
+}
+
+// ------------------------------------------------------------------------------------------------
+// merge prep (merging.py:79-89): out = [proj[b,0] | proj[b,n] - proj[b,0]]
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+__global__ void merge_prep_kernel(int B, int N, int hw, int C, dbsr_tensor proj, dbsr_tensor out) {
+    const int groups = C / 8;
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long long)B * N * hw * groups) return;
+    const int g = (int)(idx % groups);
+    const long long pix = idx / groups;
+    const int f = (int)(pix / hw), rr = (int)(pix - (long long)f * hw);
+    const int b = f / N;
+    float base[8], cur[8];
+    load8(img_ptr<T>(proj, b * N) + (long long)rr * proj.ld + g * 8, base);
+    load8(img_ptr<T>(proj, f) + (long long)rr * proj.ld + g * 8, cur);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) cur[j] -= base[j];
+    T* o = img_ptr<T>(out, f) + (long long)rr * out.ld + g * 8;
+    store8(o, base);
+    store8(o + C, cur);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Gaussian blur (upsampling.py:59-65): per-channel 3x3 cross-correlation with zero padding.
+// ------------------------------------------------------------------------------------------------
+struct K9 {
+    float k[9];
+};
+template <typename T>
+__global__ void blur3_kernel(int n, int h, int w, int groups, dbsr_tensor in, K9 kk, dbsr_tensor out) {
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long long)n * h * w * groups) return;
+    const int g = (int)(idx % groups);
+    const long long pix = idx / groups;
+    const int f = (int)(pix / (h * w)), rr = (int)(pix - (long long)f * h * w);
+    const int y = rr / w, x = rr - y * w;
+    const T* base = img_ptr<T>(in, f) + g * 8;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const int yy = y + i - 1;
+        if ((unsigned)yy >= (unsigned)h) continue;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int xx = x + j - 1;
+            if ((unsigned)xx >= (unsigned)w) continue;
+            float v[8];
+            load8(base + ((long long)yy * w + xx) * in.ld, v);
+            const float kv = kk.k[i * 3 + j];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) acc[q] = fmaf(kv, v[q], acc[q]);
+        }
+    }
+    store8(img_ptr<T>(out, f) + (long long)rr * out.ld + g * 8, acc);
+}
+
+inline unsigned nblocks(long long total, int bs) { return (unsigned)((total + bs - 1) / bs); }
+bool map_ok(const dbsr_tensor& t) { return t.ptr && t.map.fpg > 0; }
+bool vec_ok(const dbsr_tensor& t, int v) { return t.ld % v == 0 && t.c0 % v == 0; }
+
+template <typename F>
+int by_dtype(int dtype, F&& f) {
+    if (dtype == DBSR_BF16) return f((bf16_t*)nullptr);
+    if (dtype == DBSR_F32) return f((float*)nullptr);
+    dbsr_set_error("unsupported dtype %d", dtype);
+    return DBSR_E_ARG;
+}
+
+}  // namespace
+
+extern "C" int dbsr_warp_bilinear(int n, int h, int w, int c, dbsr_tensor feat, const float* flow,
+                                  long long flow_img_stride, dbsr_tensor out, void* stream) {
+    DBSR_CHECK_ARG(map_ok(feat) && map_ok(out) && flow, "warp: bad tensor");
+    DBSR_CHECK_ARG(feat.dtype == out.dtype, "warp: dtype mismatch");
+    DBSR_CHECK_ARG(n > 0 && h > 0 && w > 0 && c > 0 && c % 8 == 0, "warp: c must be a multiple of 8");
+    DBSR_CHECK_ARG(vec_ok(feat, 8) && vec_ok(out, 8), "warp: ld/c0 must be multiples of 8");
+    const int groups = c / 8;
+    return by_dtype(feat.dtype, [&](auto* tag) {
+        using T = std::remove_pointer_t<decltype(tag)>;
+        hipLaunchKernelGGL(warp_kernel<T>, dim3(nblocks((long long)n * h * w * groups, 256)), dim3(256), 0,
+                           (hipStream_t)stream, n, h, w, groups, feat, flow, flow_img_stride, out);
+        DBSR_LAUNCH_CHECK();
+        return 0;
+    });
+}
+
+extern "C" int dbsr_fuse_softmax(int B, int N, int hw, int c, dbsr_tensor logits, dbsr_tensor ref, dbsr_tensor oth,
+                                 dbsr_tensor fused, dbsr_tensor weights, void* stream) {
+    DBSR_CHECK_ARG(map_ok(logits) && map_ok(ref) && map_ok(fused) && (N == 1 || map_ok(oth)), "fuse: bad tensor");
+    DBSR_CHECK_ARG(logits.dtype == ref.dtype && fused.dtype == ref.dtype && (N == 1 || oth.dtype == ref.dtype),
+                   "fuse: dtype mismatch");
+    DBSR_CHECK_ARG(B > 0 && N > 0 && N <= 16 && hw > 0 && c % 4 == 0, "fuse: N must be in [1,16], c multiple of 4");
+    DBSR_CHECK_ARG(vec_ok(logits, 4) && vec_ok(ref, 4) && vec_ok(fused, 4) && (N == 1 || vec_ok(oth, 4)),
+                   "fuse: ld/c0 must be multiples of 4");
+    if (weights.ptr) DBSR_CHECK_ARG(map_ok(weights) && vec_ok(weights, 4), "fuse: bad weights tensor");
+    const int groups = c / 4;
+    const long long total = (long long)B * hw * groups;
+    return by_dtype(ref.dtype, [&](auto* tag) {
+        using T = std::remove_pointer_t<decltype(tag)>;
+        if (N <= 4)
+            hipLaunchKernelGGL((fuse_softmax_kernel<T, 4>), dim3(nblocks(total, 256)), dim3(256), 0,
+                               (hipStream_t)stream, B, N, hw, groups, logits, ref, oth, fused, weights);
+        else if (N <= 8)
+            hipLaunchKernelGGL((fuse_softmax_kernel<T, 8>), dim3(nblocks(total, 256)), dim3(256), 0,
+                               (hipStream_t)stream, B, N, hw, groups, logits, ref, oth, fused, weights);
+        else
+            hipLaunchKernelGGL((fuse_softmax_kernel<T, 16>), dim3(nblocks(total, 256)), dim3(256), 0,
+                               (hipStream_t)stream, B, N, hw, groups, logits, ref, oth, fused, weights);
+        DBSR_LAUNCH_CHECK();
+        return 0;
+    });
+}
+
+extern "C" int dbsr_merge_prep(int B, int N, int hw, int c, dbsr_tensor proj, dbsr_tensor out, void* stream) {
+    DBSR_CHECK_ARG(map_ok(proj) && map_ok(out) && proj.dtype == out.dtype, "merge_prep: bad tensor");
+    DBSR_CHECK_ARG(c % 8 == 0 && vec_ok(proj, 8) && vec_ok(out, 8) && out.c0 + 2 * c <= out.ld, "merge_prep: layout");
+    const long long total = (long long)B * N * hw * (c / 8);
+    return by_dtype(out.dtype, [&](auto* tag) {
+        using T = std::remove_pointer_t<decltype(tag)>;
+        hipLaunchKernelGGL(merge_prep_kernel<T>, dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, B, N,
+                           hw, c, proj, out);
+        DBSR_LAUNCH_CHECK();
+        return 0;
+    });
+}
+
+extern "C" int dbsr_gauss_blur3(int n, int h, int w, int c, dbsr_tensor in, const float* k_host, dbsr_tensor out,
+                                void* stream) {
+    DBSR_CHECK_ARG(map_ok(in) && map_ok(out) && k_host && in.dtype == out.dtype, "blur: bad tensor");
+    DBSR_CHECK_ARG(c % 8 == 0 && vec_ok(in, 8) && vec_ok(out, 8), "blur: layout");
+    K9 kk;
+    for (int i = 0; i < 9; ++i) kk.k[i] = k_host[i];
+    const long long total = (long long)n * h * w * (c / 8);
+    return by_dtype(in.dtype, [&](auto* tag) {
+        using T = std::remove_pointer_t<decltype(tag)>;
+        hipLaunchKernelGGL(blur3_kernel<T>, dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, n, h, w,
+                           c / 8, in, kk, out);
+        DBSR_LAUNCH_CHECK();
+        return 0;
+    });
+}

@@ -1,0 +1,520 @@
+"""Forward engine: turns a DBSRNet (parameter tree) into a plan of C-ABI kernel launches.
+
+Per (B, N, H, W, dtype, device) the engine builds a Plan once:
+  * persistent channels-last (NHWC) workspace buffers, zero-initialised so that channel padding is
+    zero forever (kernels never write pad channels);
+  * packed MFMA weights for every conv (dbsr_conv_pack_weights), done once per weight version;
+  * a list of prebuilt ctypes argument tuples, one per kernel launch (~140 launches at N=14),
+    all on the caller's current stream.
+`run()` replays that list; with use_graph the list is captured once into a HIP graph
+(torch.cuda.CUDAGraph over the current stream) and replayed as one launch.
+
+Layout map (reference file:line per stage):
+  raw     [F,H,W,8]        packed RAW, F = B*N frames              encoders.py:66
+  rgb     [F,Hp,Wp,8]      x_rgb resized to a multiple of 64       encoders.py:52, pwcnet.py:262-271
+  L1..L6  [F,h,w,C8]       PWC pyramid, computed ONCE per frame (the reference recomputes the
+                           reference frame's pyramid for each of its N-1 pairs, encoders.py:53)
+  D_l     [P,h,w,448+base] PWC decoder DenseNet buffer; each conv writes its channel slice and
+                           reads a channel suffix, so torch.cat never happens (pwcnet.py:173-177)
+  E       [F,H,W,512]      frame embeddings                         encoders.py:66-72
+  Wf      [P,H,W,512]      warped embeddings of frames 1..N-1      encoders.py:80
+  LG      [F,H,W,512]      fusion logits                            merging.py:113
+  FW      [F,H,W,512]      fusion weights (aux output)              merging.py:118
+  FUS     [B,H,W,512]      fused embedding                          merging.py:124
+  S*      [B,sH,sW,32]     post-upsampler features                  decoders.py:58-60
+"""
+import ctypes
+import math
+
+import torch
+
+from . import _lib as L
+from ._lib import IDENTITY
+
+BACKWARP_SCALE = {5: 0.625, 4: 1.25, 3: 2.5, 2: 5.0}      # fltBackwarp, pwcnet.py:121
+PWC_LEVEL_CH = {1: 16, 2: 32, 3: 64, 4: 96, 5: 128, 6: 196}
+DENSE_OUT = [128, 128, 96, 64, 32]                         # pwcnet.py:123-146
+DENSE_OFF = [320, 192, 96, 32, 0]                          # channel slice of each dense conv output
+BASE_OFF = 448                                             # = sum(DENSE_OUT)
+
+
+def r8(c):
+    return (c + 7) // 8 * 8
+
+
+def gauss_kernel3(sd, ksz=3):
+    """PixShuffleUpsampler._get_gaussian_kernel (upsampling.py:24-29) via gauss_2d (filtering.py:20-40)."""
+    k = torch.arange(-(ksz - 1) / 2, (ksz + 1) / 2, dtype=torch.float32).reshape(1, -1)
+    g1 = torch.exp(-1.0 / (2 * sd ** 2) * k ** 2) / (math.sqrt(2 * math.pi) * sd)
+    K = g1.reshape(1, 1, -1) * g1.reshape(1, -1, 1)
+    K = K / K.sum()
+    return [float(v) for v in K.reshape(-1)]
+
+
+class NHWC:
+    """Persistent buffer of n images of h x w pixels with ld elements per pixel."""
+    def __init__(self, n, h, w, ld, dtype, device):
+        self.n, self.h, self.w, self.ld, self.dtype = n, h, w, ld, dtype
+        self.t = torch.zeros(n, h, w, ld, dtype=dtype, device=device)
+
+    def d(self, c0=0, fmap=IDENTITY):
+        return L.tensor_desc(self.t, self.ld, c0, img_stride=self.h * self.w * self.ld, fmap=fmap)
+
+
+class PackedConv:
+    """One nn.Conv2d packed for dbsr_conv2d."""
+    def __init__(self, conv, dtype, device, stream, shuffle=1):
+        w = conv.weight.detach().to(device=device, dtype=torch.float32).contiguous()
+        b = conv.bias.detach().to(device=device, dtype=torch.float32).contiguous() if conv.bias is not None else None
+        self.cout, self.cin, self.kh, self.kw = w.shape
+        self.stride, self.pad, self.dil = conv.stride[0], conv.padding[0], conv.dilation[0]
+        n = L.lib().dbsr_conv_packed_elems(self.cout, self.cin, self.kh, self.kw)
+        self.w = torch.empty(n, dtype=dtype, device=device)
+        self.bias = torch.empty(self.cout, dtype=torch.float32, device=device) if b is not None else None
+        L.check(L.lib().dbsr_conv_pack_weights(w.data_ptr(), b.data_ptr() if b is not None else None, self.cout,
+                                               self.cin, self.kh, self.kw, L.dtype_code(dtype), shuffle,
+                                               self.w.data_ptr(),
+                                               self.bias.data_ptr() if self.bias is not None else None, stream),
+                'dbsr_conv_pack_weights')
+        self._keep = (w, b)
+
+    def out_hw(self, h, w):
+        return ((h + 2 * self.pad - self.dil * (self.kh - 1) - 1) // self.stride + 1,
+                (w + 2 * self.pad - self.dil * (self.kw - 1) - 1) // self.stride + 1)
+
+
+class Plan:
+    def __init__(self):
+        self.ops = []        # (callable, args, name)
+        self.keep = []
+        self.work = {}       # op index -> ('flop' | 'byte', algorithmic amount per launch)
+
+    def add(self, name, fn, *args, work=None):
+        if work is not None:
+            self.work[len(self.ops)] = work
+        self.ops.append((fn, args, name))
+
+    def conv(self, name, pc, n_frames, x, xc0, in_hw, y, yc0, act, xmap=IDENTITY, ymap=IDENTITY, res=None,
+             rc0=0, rmap=IDENTITY, post_act=L.ACT_NONE, out_mode=L.OUT_NHWC, shuffle=0, y_desc=None, cin=None):
+        oh, ow = pc.out_hw(*in_hw)
+        assert cin is None or cin == pc.cin, (name, cin, pc.cin)
+        d = L.ConvDesc()
+        d.n_frames = n_frames
+        d.x = x.d(xc0, xmap)
+        d.in_h, d.in_w = in_hw
+        d.cin = pc.cin if cin is None else cin
+        d.w = pc.w.data_ptr()
+        d.bias = pc.bias.data_ptr() if pc.bias is not None else None
+        d.cout, d.kh, d.kw, d.stride, d.pad, d.dil = pc.cout, pc.kh, pc.kw, pc.stride, pc.pad, pc.dil
+        d.y = y_desc if y_desc is not None else y.d(yc0, ymap)
+        d.out_h, d.out_w = oh, ow               # (OUT_SHUFFLE: the kernel scales by `shuffle` itself)
+        d.act = act
+        d.res = res.d(rc0, rmap) if res is not None else L.NULL_TENSOR
+        d.post_act = post_act
+        d.out_mode, d.shuffle = out_mode, shuffle
+        self.keep.append(d)
+        flop = 2.0 * n_frames * oh * ow * pc.cout * d.cin * pc.kh * pc.kw
+        self.add(name, L.lib().dbsr_conv2d, ctypes.byref(d), work=('flop', flop))
+        return d
+
+    def run(self, stream):
+        for fn, args, name in self.ops:
+            rc = fn(*args, stream)
+            if rc != 0:
+                L.check(rc, name)
+
+    def time_ops(self, stream, reps=10):
+        """Average device time (ms) of each op, each launched `reps` times back to back between two
+        HIP events on `stream` (the stream the ops run on)."""
+        out = []
+        for fn, args, name in self.ops:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            fn(*args, stream)
+            e0.record()
+            for _ in range(reps):
+                fn(*args, stream)
+            e1.record()
+            e1.synchronize()
+            out.append((name, e0.elapsed_time(e1) / reps))
+        return out
+
+
+class _Weights:
+    """All packed weights of a DBSRNet / PWCNet for one (dtype, device)."""
+    def __init__(self, dtype, device, stream):
+        self.dtype, self.device, self.stream = dtype, device, stream
+
+    def conv(self, module, shuffle=1):
+        return PackedConv(module, self.dtype, self.device, self.stream, shuffle=shuffle)
+
+
+def _param_signature(module):
+    return tuple((p.data_ptr(), p._version) for p in module.parameters())
+
+
+# ==================================================================================================
+# PWC-Net sub-plan
+# ==================================================================================================
+class PWCPlanner:
+    """Packs PWC-Net weights and emits the PWC part of a plan (pwcnet.py:221-231 + :262-279)."""
+    def __init__(self, pwc_module, W):
+        net = pwc_module.net
+        ex = net.netExtractor
+        self.ext = []
+        for lvl in ['netOne', 'netTwo', 'netThr', 'netFou', 'netFiv', 'netSix']:
+            seq = getattr(ex, lvl)
+            self.ext.append([W.conv(seq[0]), W.conv(seq[2]), W.conv(seq[4])])
+        self.dec = {}
+        for level, name in zip([2, 3, 4, 5, 6], ['netTwo', 'netThr', 'netFou', 'netFiv', 'netSix']):
+            d = getattr(net, name)
+            ent = {'dense': [W.conv(getattr(d, n)[0]) for n in ['netOne', 'netTwo', 'netThr', 'netFou', 'netFiv']],
+                   'flow': W.conv(d.netSix[0])}
+            if level < 6:
+                ent['upflow'] = (d.netUpflow.weight.detach().to(W.device, torch.float32).contiguous(),
+                                 d.netUpflow.bias.detach().to(W.device, torch.float32).contiguous())
+                ent['upfeat'] = (d.netUpfeat.weight.detach().to(W.device, torch.float32).contiguous(),
+                                 d.netUpfeat.bias.detach().to(W.device, torch.float32).contiguous())
+            self.dec[level] = ent
+        self.ref = [W.conv(net.netRefiner.netMain[i]) for i in range(0, 13, 2)]
+
+    def build(self, plan, dtype, device, nF, Hp, Wp, P, first_map, second_map, rgb, flow_out):
+        """Emit: extractor over the nF frames stored in `rgb` ([nF,Hp,Wp,8]); decoders over P pairs whose
+        first/second features are frames first_map(p) / second_map(p); refined flow (fp32, 2 ch) into
+        `flow_out` ([P,Hp/4,Wp/4,2])."""
+        lib = L.lib()
+        # ---- feature pyramid (Extractor.forward, pwcnet.py:103-111), once per frame ----
+        levels = {}
+        x, hw = rgb, (Hp, Wp)
+        for k in range(6):
+            C = PWC_LEVEL_CH[k + 1]
+            oh, ow = self.ext[k][0].out_hw(*hw)
+            ta = NHWC(nF, oh, ow, r8(C), dtype, device)
+            tb = NHWC(nF, oh, ow, r8(C), dtype, device)
+            lv = NHWC(nF, oh, ow, r8(C), dtype, device)
+            plan.conv(f'pwc.ext{k + 1}.0', self.ext[k][0], nF, x, 0, hw, ta, 0, L.ACT_LRELU)
+            plan.conv(f'pwc.ext{k + 1}.2', self.ext[k][1], nF, ta, 0, (oh, ow), tb, 0, L.ACT_LRELU)
+            plan.conv(f'pwc.ext{k + 1}.4', self.ext[k][2], nF, tb, 0, (oh, ow), lv, 0, L.ACT_LRELU)
+            levels[k + 1] = lv
+            x, hw = lv, (oh, ow)
+        plan.keep.append(levels)
+        # ---- decoders, coarse to fine (pwcnet.py:225-229, Decoder.forward :153-184) ----
+        prev = None
+        for level in [6, 5, 4, 3, 2]:
+            feat = levels[level]
+            h, w, C = feat.h, feat.w, PWC_LEVEL_CH[level]
+            base_real = 81 if level == 6 else 81 + C + 4
+            ld = BASE_OFF + r8(base_real)
+            D = NHWC(P, h, w, ld, dtype, device)
+            ent = self.dec[level]
+            if prev is None:
+                second = feat.d(0, second_map)
+            else:
+                pD, pflow, pbase = prev
+                fu = NHWC(P, h, w, 2, torch.float32, device)     # upflow
+                fe = NHWC(P, h, w, 2, torch.float32, device)     # upfeat
+                wt, bs = ent['upflow']
+                plan.add(f'pwc.dec{level}.upflow', lib.dbsr_conv_transpose_k4s2, P, pD.h, pD.w, 2, 2, pflow.d(0),
+                         wt.data_ptr(), bs.data_ptr(), fu.d(0))
+                wt, bs = ent['upfeat']
+                plan.add(f'pwc.dec{level}.upfeat', lib.dbsr_conv_transpose_k4s2, P, pD.h, pD.w, BASE_OFF + pbase, 2,
+                         pD.d(0), wt.data_ptr(), bs.data_ptr(), fe.d(0))
+                ws = NHWC(P, h, w, r8(C), dtype, device)
+                plan.add(f'pwc.dec{level}.backwarp', lib.dbsr_backwarp, P, h, w, C, feat.d(0, second_map), fu.d(0),
+                         BACKWARP_SCALE[level], ws.d(0))
+                plan.add(f'pwc.dec{level}.assemble', lib.dbsr_pwc_assemble, P, h, w, C, feat.d(0, first_map), fu.d(0),
+                         fe.d(0), D.d(BASE_OFF))
+                second = ws.d(0)
+                plan.keep.extend([fu, fe, ws])
+            plan.add(f'pwc.dec{level}.corr', lib.dbsr_correlation, P, h, w, C, feat.d(0, first_map), second,
+                     D.d(BASE_OFF), 1)
+            cin = base_real
+            for i, (pc, off) in enumerate(zip(ent['dense'], DENSE_OFF)):
+                start = BASE_OFF if i == 0 else DENSE_OFF[i - 1]
+                plan.conv(f'pwc.dec{level}.dense{i}', pc, P, D, start, (h, w), D, off, L.ACT_LRELU, cin=cin)
+                cin += DENSE_OUT[i]
+            fl = NHWC(P, h, w, 2, torch.float32, device)
+            plan.conv(f'pwc.dec{level}.flow', ent['flow'], P, D, 0, (h, w), None, 0, L.ACT_NONE, cin=cin,
+                      y_desc=fl.d(0))
+            plan.keep.extend([D, fl])
+            prev = (D, fl, base_real)
+        # ---- refiner (pwcnet.py:186-207) + residual flow (:231) ----
+        D2, fl2, base2 = prev
+        h, w = D2.h, D2.w
+        chans = [128, 128, 128, 96, 64, 32]
+        bufs = [NHWC(P, h, w, r8(c), dtype, device) for c in chans]
+        x, xc0, cin = D2, 0, BASE_OFF + base2
+        for i in range(6):
+            plan.conv(f'pwc.refiner{i}', self.ref[i], P, x, xc0, (h, w), bufs[i], 0, L.ACT_LRELU, cin=cin)
+            x, xc0, cin = bufs[i], 0, chans[i]
+        plan.conv('pwc.refiner6', self.ref[6], P, x, 0, (h, w), None, 0, L.ACT_NONE, y_desc=flow_out.d(0),
+                  res=fl2)
+        plan.keep.extend(bufs)
+
+
+# ==================================================================================================
+# DBSR engine
+# ==================================================================================================
+class DBSREngine:
+    def __init__(self, net):
+        self.net = net
+        self.dtype = net.compute_dtype
+        self.device = None
+        self.sig = None
+        self.plans = {}
+        self.graphs = {}
+
+    def matches(self, net):
+        return net is self.net and self.dtype == net.compute_dtype and self.sig == _param_signature(net)
+
+    def _pack(self, device):
+        net = self.net
+        stream = L.stream_ptr(device)
+        W = _Weights(self.dtype, device, stream)
+        enc, mer, dec = net.encoder, net.merging, net.decoder
+        self.pwc = PWCPlanner(enc.alignment_net, W)
+        self.enc_init = W.conv(enc.init_layer[0])
+        self.enc_res = [(W.conv(b.conv1[0]), W.conv(b.conv2[0])) for b in enc.res_layers]
+        self.enc_out = W.conv(enc.out_layer[0])
+        self.proj = W.conv(mer.feat_project_layer[0])
+        ofe = list(mer.offset_feat_extractor)
+        self.ofe_init = W.conv(ofe[0][0])
+        self.ofe_res = [(W.conv(b.conv1[0]), W.conv(b.conv2[0])) for b in ofe[1:]]
+        wp = list(mer.weight_predictor)
+        self.wp_init = W.conv(wp[0][0])
+        self.wp_res = [(W.conv(b.conv1[0]), W.conv(b.conv2[0])) for b in wp[1:-1]]
+        self.wp_out = W.conv(wp[-1][0])
+        self.dec_init = W.conv(dec.init_layer[0])
+        self.dec_pre = [(W.conv(b.conv1[0]), W.conv(b.conv2[0])) for b in dec.pre_res_layers]
+        up = dec.upsample_layer
+        self.s = up.upsample_factor
+        self.dec_up = W.conv(up.conv_layer[0], shuffle=self.s)
+        self.blur = gauss_kernel3(up.gauss_blur_sd, up.gauss_ksz) if up.gauss_blur_sd is not None else None
+        if self.blur is not None and up.gauss_ksz != 3:
+            raise NotImplementedError('gauss_ksz != 3')
+        self.dec_post = [(W.conv(b.conv1[0]), W.conv(b.conv2[0])) for b in dec.post_res_layers]
+        self.pred = W.conv(dec.predictor[0])
+        self.device = device
+        self.sig = _param_signature(net)
+        self.plans, self.graphs = {}, {}
+
+    def _resblocks(self, plan, name, blocks, n, hw, bufs, x_idx, dtype):
+        """ResBlock chain (blocks.py:81-96) over ping-pong buffers; returns index of the result buffer."""
+        a = x_idx
+        for i, (c1, c2) in enumerate(blocks):
+            b, c = [j for j in range(3) if j != a]
+            plan.conv(f'{name}{i}.conv1', c1, n, bufs[a], 0, hw, bufs[b], 0, L.ACT_RELU)
+            plan.conv(f'{name}{i}.conv2', c2, n, bufs[b], 0, hw, bufs[c], 0, L.ACT_NONE, res=bufs[a],
+                      post_act=L.ACT_RELU)
+            a = c
+        return a
+
+    def _build(self, B, N, H, W):
+        dt, dev = self.dtype, self.device
+        lib = L.lib()
+        plan = Plan()
+        F, P = B * N, B * (N - 1)
+        C = self.enc_out.cout
+        hw = (H, W)
+        S = self.s
+        bufs = {}
+        bufs['burst'] = torch.zeros(B, N, 4, H, W, dtype=torch.float32, device=dev)
+        raw = NHWC(F, H, W, 8, dt, dev)
+        Hp, Wp = int(math.ceil(H / 64.0) * 64), int(math.ceil(W / 64.0) * 64)
+        rgb = NHWC(F, Hp, Wp, 8, dt, dev)
+        bufs['offsets'] = torch.zeros(P, 2, H, W, dtype=torch.float32, device=dev)
+        om = NHWC(F, H, W, 8, dt, dev)
+        zero_flow = getattr(self.net, 'zero_flow', False)
+        plan.add('pack_burst', lib.dbsr_pack_burst, B, N, H, W, bufs['burst'].data_ptr(), raw.d(0), Hp, Wp,
+                 rgb.d(0) if not zero_flow else L.NULL_TENSOR)
+        # ---------------- alignment (PWC-Net) ----------------
+        if not zero_flow:
+            flow_out = NHWC(P, Hp // 4, Wp // 4, 2, torch.float32, dev)
+            self.pwc.build(plan, dt, dev, F, Hp, Wp, P, first_map=(N - 1, N, 0, 0), second_map=(N - 1, N, 1, 1),
+                           rgb=rgb, flow_out=flow_out)
+            plan.add('flow_finalize', lib.dbsr_flow_finalize, B, N, Hp // 4, Wp // 4, flow_out.d(0), H, W, Hp, Wp,
+                     bufs['offsets'].data_ptr(), 1.0, om.d(0))
+            plan.keep.append(flow_out)
+        # (zero flow: offsets and om stay zero from initialisation)
+        # ---------------- encoder (encoders.py:66-72) ----------------
+        e = [NHWC(F, H, W, r8(self.enc_init.cout), dt, dev) for _ in range(3)]
+        plan.conv('enc.init', self.enc_init, F, raw, 0, hw, e[0], 0, L.ACT_RELU)
+        i = self._resblocks(plan, 'enc.res', self.enc_res, F, hw, e, 0, dt)
+        E = NHWC(F, H, W, C, dt, dev)
+        plan.conv('enc.out', self.enc_out, F, e[i], 0, hw, E, 0, L.ACT_RELU)
+        # ---------------- warp (encoders.py:80) ----------------
+        Wf = NHWC(max(P, 1), H, W, C, dt, dev)
+        es = 2 if dt == torch.bfloat16 else 4
+        if P > 0:
+            plan.add('warp', lib.dbsr_warp_bilinear, P, H, W, C, E.d(0, (N - 1, N, 1, 1)), bufs['offsets'].data_ptr(),
+                     2 * H * W, Wf.d(0), work=('byte', 2.0 * P * C * H * W * es + 8.0 * P * H * W))
+        # ---------------- merging (merging.py:61-127) ----------------
+        pd = self.proj.cout
+        PJ = NHWC(F, H, W, r8(pd), dt, dev)
+        plan.conv('merge.proj_ref', self.proj, B, E, 0, hw, PJ, 0, L.ACT_RELU, xmap=(1, N, 0, 1), ymap=(1, N, 0, 1))
+        if P > 0:
+            plan.conv('merge.proj_oth', self.proj, P, Wf, 0, hw, PJ, 0, L.ACT_RELU, ymap=(N - 1, N, 1, 1))
+        od = self.ofe_init.cout
+        WP = NHWC(F, H, W, 2 * pd + od, dt, dev)
+        plan.add('merge.prep', lib.dbsr_merge_prep, B, N, H * W, pd, PJ.d(0), WP.d(0))
+        o = [NHWC(F, H, W, od, dt, dev) for _ in range(3)]
+        plan.conv('merge.ofe.init', self.ofe_init, F, om, 0, hw, o[0], 0, L.ACT_RELU)
+        a = 0
+        for k, (c1, c2) in enumerate(self.ofe_res):
+            b, c = [j for j in range(3) if j != a]
+            last = k == len(self.ofe_res) - 1
+            plan.conv(f'merge.ofe.res{k}.conv1', c1, F, o[a], 0, hw, o[b], 0, L.ACT_RELU)
+            if last:
+                plan.conv(f'merge.ofe.res{k}.conv2', c2, F, o[b], 0, hw, WP, 2 * pd, L.ACT_NONE, res=o[a],
+                          post_act=L.ACT_RELU)
+            else:
+                plan.conv(f'merge.ofe.res{k}.conv2', c2, F, o[b], 0, hw, o[c], 0, L.ACT_NONE, res=o[a],
+                          post_act=L.ACT_RELU)
+                a = c
+        if not self.ofe_res:
+            raise NotImplementedError('num_offset_feat_extractor_res must be >= 1')
+        q = [NHWC(F, H, W, self.wp_init.cout, dt, dev) for _ in range(3)]
+        plan.conv('merge.wp.init', self.wp_init, F, WP, 0, hw, q[0], 0, L.ACT_RELU)
+        i = self._resblocks(plan, 'merge.wp.res', self.wp_res, F, hw, q, 0, dt)
+        LG = NHWC(F, H, W, C, dt, dev)
+        plan.conv('merge.wp.out', self.wp_out, F, q[i], 0, hw, LG, 0, L.ACT_NONE)
+        FUS = NHWC(B, H, W, C, dt, dev)
+        FW = NHWC(F, H, W, C, dt, dev)
+        bufs['fw_desc'] = FW.d(0)
+        fuse_args = [B, N, H * W, C, LG.d(0), E.d(0, (1, N, 0, 1)), Wf.d(0), FUS.d(0), FW.d(0)]
+        plan.add('merge.fuse', lib.dbsr_fuse_softmax, *fuse_args)
+        fuse_idx = len(plan.ops) - 1
+        plan.fuse_bytes = ((2.0 * N + 1) * B * C * H * W * es, 1.0 * N * B * C * H * W * es)
+        # ---------------- decoder (decoders.py:54-62) ----------------
+        gd = self.dec_init.cout
+        g = [NHWC(B, H, W, gd, dt, dev) for _ in range(3)]
+        plan.conv('dec.init', self.dec_init, B, FUS, 0, hw, g[0], 0, L.ACT_RELU)
+        i = self._resblocks(plan, 'dec.pre', self.dec_pre, B, hw, g, 0, dt)
+        pc = self.dec_up.cout // (S * S)
+        sh = [NHWC(B, H * S, W * S, pc, dt, dev) for _ in range(3)]
+        plan.conv('dec.upsample', self.dec_up, B, g[i], 0, hw, sh[0], 0, L.ACT_RELU, out_mode=L.OUT_SHUFFLE,
+                  shuffle=S)
+        a = 0
+        if self.blur is not None:
+            kbuf = (ctypes.c_float * 9)(*self.blur)
+            plan.keep.append(kbuf)
+            plan.add('dec.blur', lib.dbsr_gauss_blur3, B, H * S, W * S, pc, sh[0].d(0), kbuf, sh[1].d(0))
+            a = 1
+        i = self._resblocks(plan, 'dec.post', self.dec_post, B, (H * S, W * S), sh, a, dt)
+        bufs['pred'] = torch.zeros(B, 3, H * S, W * S, dtype=torch.float32, device=dev)
+        pdesc = L.tensor_desc(bufs['pred'], 1, 0, img_stride=3 * H * S * W * S, dtype=torch.float32)
+        plan.conv('dec.predictor', self.pred, B, sh[i], 0, (H * S, W * S), None, 0, L.ACT_RELU,
+                  out_mode=L.OUT_NCHW_F32, y_desc=pdesc)
+        plan.keep.extend([raw, rgb, om, e, E, Wf, PJ, WP, o, q, LG, FUS, FW, g, sh])
+        plan.bufs = bufs
+        plan.FW = FW
+        plan.fuse_idx = fuse_idx
+        plan.fuse_args = fuse_args
+        plan.shape = (B, N, H, W)
+        return plan
+
+    def _set_fw(self, plan, want):
+        fn, args, name = plan.ops[plan.fuse_idx]
+        args = list(plan.fuse_args)
+        args[-1] = plan.bufs['fw_desc'] if want else L.NULL_TENSOR
+        plan.ops[plan.fuse_idx] = (fn, tuple(args), name)
+        plan.work[plan.fuse_idx] = ('byte', plan.fuse_bytes[0] + (plan.fuse_bytes[1] if want else 0.0))
+
+    def forward(self, burst):
+        if not burst.is_cuda:
+            raise RuntimeError('DBSRNet (MI355X engine) needs the burst on a HIP device; got %s' % burst.device)
+        if burst.dim() != 5 or burst.shape[2] != 4:
+            raise ValueError('burst must be [B,N,4,H,W]')
+        B, N, _, H, W = burst.shape
+        if N < 2:
+            raise ValueError('burst needs at least 2 frames')
+        dev = burst.device
+        if self.device != dev or self.sig != _param_signature(self.net):
+            self._pack(dev)
+        key = (B, N, H, W)
+        plan = self.plans.get(key)
+        if plan is None:
+            plan = self.plans[key] = self._build(B, N, H, W)
+        want_fw = bool(getattr(self.net, 'return_fusion_weights', True))
+        self._set_fw(plan, want_fw)
+        stream = L.stream_ptr(dev)
+        plan.bufs['burst'].copy_(burst.to(torch.float32), non_blocking=True)
+        if getattr(self.net, 'use_graph', False):
+            g = self.graphs.get((key, want_fw))
+            if g is None:
+                plan.run(stream)                      # warm-up outside capture
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    plan.run(L.stream_ptr(dev))
+                self.graphs[(key, want_fw)] = g
+            g.replay()
+            pred, offs = plan.bufs['pred'], plan.bufs['offsets']
+            fw_t = plan.FW.t
+        else:
+            plan.run(stream)
+            pred, offs = plan.bufs['pred'].clone(), plan.bufs['offsets'].clone()
+            fw_t = plan.FW.t.clone() if want_fw else None
+        aux = {'offsets': offs.view(B, N - 1, 2, H, W)}
+        if want_fw:
+            # [B*N,H,W,C] channels-last storage viewed as the reference's [B,N,C,H,W]
+            aux['fusion_weights'] = fw_t.view(B, N, H, W, -1).permute(0, 1, 4, 2, 3)
+        else:
+            aux['fusion_weights'] = None
+        return pred, aux
+
+
+# ==================================================================================================
+# standalone PWC-Net (the alignment sub-seam, pwcnet.py:248-281)
+# ==================================================================================================
+class PWCEngine:
+    def __init__(self, module):
+        self.module = module
+        self.dtype = module.compute_dtype
+        self.sig = None
+        self.device = None
+        self.plans = {}
+
+    def matches(self, module):
+        return module is self.module and self.dtype == module.compute_dtype and self.sig == _param_signature(module)
+
+    def forward(self, source_img, target_img):
+        if not source_img.is_cuda:
+            raise RuntimeError('PWCNet (MI355X engine) needs inputs on a HIP device')
+        H, W = source_img.shape[-2:]
+        src = source_img.reshape(-1, 3, H, W)
+        tgt = target_img.reshape(-1, 3, H, W)
+        if self.module.rgb2bgr:
+            src, tgt = src[:, [2, 1, 0]], tgt[:, [2, 1, 0]]
+        P = src.shape[0]
+        dev = src.device
+        if self.device != dev or self.sig != _param_signature(self.module):
+            self.pwc = PWCPlanner(self.module, _Weights(self.dtype, dev, L.stream_ptr(dev)))
+            self.device, self.sig, self.plans = dev, _param_signature(self.module), {}
+        key = (P, H, W)
+        plan = self.plans.get(key)
+        lib = L.lib()
+        if plan is None:
+            plan = Plan()
+            Hp, Wp = int(math.ceil(H / 64.0) * 64), int(math.ceil(W / 64.0) * 64)
+            # frames 0..P-1 = target (tenFirst), P..2P-1 = source (tenSecond): pwcnet.py:273
+            inp = torch.zeros(2 * P, 1, 4, H, W, dtype=torch.float32, device=dev)
+            rgb = NHWC(2 * P, Hp, Wp, 8, self.dtype, dev)
+            flow_out = NHWC(P, Hp // 4, Wp // 4, 2, torch.float32, dev)
+            offs = torch.zeros(P, 2, H, W, dtype=torch.float32, device=dev)
+            plan.add('pack_rgb', lib.dbsr_pack_burst, 2 * P, 1, H, W, inp.data_ptr(), L.NULL_TENSOR, Hp, Wp, rgb.d(0))
+            self.pwc.build(plan, self.dtype, dev, 2 * P, Hp, Wp, P, first_map=IDENTITY, second_map=(1, 1, P, 1),
+                           rgb=rgb, flow_out=flow_out)
+            # B = P bursts of N = 2 frames -> pair p = burst p
+            plan.add('flow_finalize', lib.dbsr_flow_finalize, P, 2, Hp // 4, Wp // 4, flow_out.d(0), H, W, Hp, Wp,
+                     offs.data_ptr(), 1.0, L.NULL_TENSOR)
+            plan.keep.extend([rgb, flow_out])
+            plan.inp, plan.offs = inp, offs
+            self.plans[key] = plan
+        # pack_burst expects 4 planes (R, G1, G2, B) -> put G in both green planes so mean(G1,G2) = G
+        v = plan.inp.view(2, P, 4, H, W)
+        for dst, srcimg in ((v[0], tgt), (v[1], src)):
+            dst[:, 0] = srcimg[:, 0]
+            dst[:, 1] = srcimg[:, 1]
+            dst[:, 2] = srcimg[:, 1]
+            dst[:, 3] = srcimg[:, 2]
+        plan.run(L.stream_ptr(dev))
+        return plan.offs.clone()

@@ -1,0 +1,121 @@
+"""Op-level mirror of the reference's functional sub-seams, NCHW in / NCHW out like the reference:
+
+  FunctionCorrelation(tenFirst, tenSecond)      external/pwcnet/correlation/correlation.py:385-387
+  backwarp(tenInput, tenFlow)                   models/alignment/pwcnet.py:16-38
+  warp(feat, flow, mode, padding_mode)          models/layers/warp.py:19-46
+  conv2d(...)                                   nn.Conv2d (+ fused activation / residual) via dbsr_conv2d
+
+Each runs the HIP kernel of libdbsr_hip.so; the NCHW<->NHWC permutes around the call are torch
+device copies (layout plumbing for callers that hold NCHW tensors; the engine never uses them).
+Errors mirror the reference: non-contiguous input to the correlation raises (correlation.py:286-287),
+a CPU tensor raises (correlation.py:324-325 raises NotImplementedError on CPU).
+"""
+import torch
+
+from . import _lib as L
+
+
+def _nhwc(x, dtype=None):
+    t = x.permute(0, 2, 3, 1)
+    if dtype is not None:
+        t = t.to(dtype)
+    c = t.shape[-1]
+    ld = (c + 7) // 8 * 8
+    out = torch.zeros(*t.shape[:-1], ld, dtype=t.dtype, device=t.device)
+    out[..., :c] = t
+    return out, ld
+
+
+def _need_cuda(*ts):
+    for t in ts:
+        if not t.is_cuda:
+            raise NotImplementedError('dbsr_amd ops run on the HIP device only (no CPU implementation, as '
+                                      'correlation.py:324-325)')
+
+
+def FunctionCorrelation(tenFirst, tenSecond, leaky=False):
+    """81-channel cost volume / C (K2).  leaky=True fuses the callers' leaky_relu(0.1)."""
+    _need_cuda(tenFirst, tenSecond)
+    if not (tenFirst.is_contiguous() and tenSecond.is_contiguous()):
+        raise AssertionError('correlation inputs must be contiguous (correlation.py:286-287)')
+    N, C, H, W = tenFirst.shape
+    dt = tenFirst.dtype
+    a, lda = _nhwc(tenFirst)
+    b, ldb = _nhwc(tenSecond)
+    out = torch.zeros(N, H, W, 88, dtype=dt, device=tenFirst.device)
+    L.check(L.lib().dbsr_correlation(N, H, W, C, L.tensor_desc(a, lda), L.tensor_desc(b, ldb),
+                                     L.tensor_desc(out, 88), 1 if leaky else 0, L.stream_ptr(tenFirst.device)),
+            'dbsr_correlation')
+    return out[..., :81].permute(0, 3, 1, 2).contiguous()
+
+
+class ModuleCorrelation(torch.nn.Module):
+    def forward(self, tenFirst, tenSecond):
+        return FunctionCorrelation(tenFirst, tenSecond)
+
+
+def backwarp(tenInput, tenFlow):
+    _need_cuda(tenInput, tenFlow)
+    N, C, H, W = tenInput.shape
+    x, ldx = _nhwc(tenInput)
+    fl = tenFlow.permute(0, 2, 3, 1).to(torch.float32).contiguous()
+    out = torch.zeros_like(x)
+    L.check(L.lib().dbsr_backwarp(N, H, W, C, L.tensor_desc(x, ldx), L.tensor_desc(fl, 2), 1.0,
+                                  L.tensor_desc(out, ldx), L.stream_ptr(tenInput.device)), 'dbsr_backwarp')
+    return out[..., :C].permute(0, 3, 1, 2).contiguous()
+
+
+def warp(feat, flow, mode='bilinear', padding_mode='zeros'):
+    if mode != 'bilinear' or padding_mode != 'zeros':
+        raise NotImplementedError('only bilinear / zeros is on the hot path (encoders.py:80)')
+    _need_cuda(feat, flow)
+    N, C, H, W = feat.shape
+    x, ld = _nhwc(feat)
+    fl = flow.to(torch.float32).contiguous()
+    out = torch.zeros_like(x)
+    L.check(L.lib().dbsr_warp_bilinear(N, H, W, ld, L.tensor_desc(x, ld), fl.data_ptr(), 2 * H * W,
+                                       L.tensor_desc(out, ld), L.stream_ptr(feat.device)), 'dbsr_warp_bilinear')
+    return out[..., :C].permute(0, 3, 1, 2).contiguous()
+
+
+def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, act=L.ACT_NONE, residual=None,
+           post_act=L.ACT_NONE, compute_dtype=torch.float32, out_f32=False):
+    """act(conv2d(x) + bias) (+ residual, then post_act); NCHW in/out, computed by dbsr_conv2d."""
+    _need_cuda(x, weight)
+    N, Cin, H, W = x.shape
+    Cout, _, kh, kw = weight.shape
+    dev = x.device
+    xs, ldx = _nhwc(x, compute_dtype)
+    n = L.lib().dbsr_conv_packed_elems(Cout, Cin, kh, kw)
+    wp = torch.empty(n, dtype=compute_dtype, device=dev)
+    bp = torch.empty(Cout, dtype=torch.float32, device=dev) if bias is not None else None
+    w32 = weight.to(torch.float32).contiguous()
+    b32 = bias.to(torch.float32).contiguous() if bias is not None else None
+    s = L.stream_ptr(dev)
+    L.check(L.lib().dbsr_conv_pack_weights(w32.data_ptr(), b32.data_ptr() if b32 is not None else None, Cout, Cin,
+                                           kh, kw, L.dtype_code(compute_dtype), 1, wp.data_ptr(),
+                                           bp.data_ptr() if bp is not None else None, s), 'pack')
+    oh = (H + 2 * padding - dilation * (kh - 1) - 1) // stride + 1
+    ow = (W + 2 * padding - dilation * (kw - 1) - 1) // stride + 1
+    ody = torch.float32 if out_f32 else compute_dtype
+    ldy = (Cout + 7) // 8 * 8
+    y = torch.zeros(N, oh, ow, ldy, dtype=ody, device=dev)
+    d = L.ConvDesc()
+    d.n_frames = N
+    d.x = L.tensor_desc(xs, ldx)
+    d.in_h, d.in_w, d.cin = H, W, Cin
+    d.w = wp.data_ptr()
+    d.bias = bp.data_ptr() if bp is not None else None
+    d.cout, d.kh, d.kw, d.stride, d.pad, d.dil = Cout, kh, kw, stride, padding, dilation
+    d.y = L.tensor_desc(y, ldy)
+    d.out_h, d.out_w = oh, ow
+    d.act = act
+    if residual is not None:
+        rr, _ = _nhwc(residual, ody)
+        d.res = L.tensor_desc(rr, ldy)
+    else:
+        d.res = L.NULL_TENSOR
+    d.post_act = post_act
+    d.out_mode, d.shuffle = L.OUT_NHWC, 0
+    L.check(L.lib().dbsr_conv2d(d, s), 'dbsr_conv2d')
+    return y[..., :Cout].permute(0, 3, 1, 2).contiguous()

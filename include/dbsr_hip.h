@@ -1,0 +1,150 @@
+/* dbsr_hip.h — C ABI of libdbsr_hip.so, the MI355X (gfx950) kernels of the DBSR forward path.
+ *
+ * Plain pointers, sizes and a hipStream_t passed as void*.  No torch types.  Every entry point
+ * returns 0 on success, a positive hipError_t on a HIP launch error, or a negative DBSR_E_* code on
+ * an argument error (dbsr_last_error() gives the message).  All pointers are device pointers unless
+ * a comment says otherwise.  Entry points are stateless and launch on the given stream only (no
+ * allocation, no synchronisation), so a caller may capture them into a hipGraph.
+ *
+ * Activation layout ("NHWC"): an image is H*W pixels, each pixel `ld` elements apart; a tensor's
+ * channels live at [c0, c0+C) of each pixel.  Images of a batch are `img_stride` elements apart and
+ * a dbsr_frame_map selects which stored image a logical frame index refers to.
+ *
+ * Reference interfaces these replace (paths relative to the reference repo):
+ *   dbsr_correlation          external/pwcnet/correlation/correlation.py:278-330 (FunctionCorrelation,
+ *                             :385) incl. the leaky_relu applied by its callers, pwcnet.py:161,169
+ *   dbsr_backwarp             models/alignment/pwcnet.py:16-38 (backwarp)
+ *   dbsr_warp_bilinear        models/layers/warp.py:19-46 (warp), called at models/dbsr/encoders.py:80
+ *   dbsr_fuse_softmax         models/dbsr/merging.py:116-126 (softmax over the burst + weighted sum)
+ *   dbsr_conv2d               nn.Conv2d (+ReLU/LeakyReLU, ResBlock residual, PixelShuffle epilogue)
+ *                             as composed by models/layers/blocks.py:46-96, upsampling.py:51-58,
+ *                             models/alignment/pwcnet.py:45-207, models/dbsr/{encoders,merging,decoders}.py
+ *   dbsr_conv_transpose_k4s2  nn.ConvTranspose2d(k=4,s=2,p=1), pwcnet.py:119-120,166-167
+ *   dbsr_pack_burst           encoders.py:52-54 (x_rgb) + pwcnet.py:262-271 (resize to a multiple of 64)
+ *   dbsr_flow_finalize        pwcnet.py:274-279 (x20 bilinear upsample + rescale) + merging.py:98-105
+ *                             (offsets_all = cat(0, offsets) % offset_modulo)
+ *   dbsr_gauss_blur3          upsampling.py:59-65 (depthwise Gaussian, zero padding)
+ *   dbsr_merge_prep           merging.py:79-89 (base_feat_proj, feat_diff_proj)
+ *   dbsr_pwc_assemble         pwcnet.py:171 (cat([tenVolume, tenFirst, tenFlow, tenFeat]))
+ */
+#ifndef DBSR_HIP_H
+#define DBSR_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DBSR_ABI_VERSION 1
+
+enum { DBSR_F32 = 0, DBSR_BF16 = 1 };
+enum { DBSR_ACT_NONE = 0, DBSR_ACT_RELU = 1, DBSR_ACT_LRELU = 2 };      /* LeakyReLU slope 0.1 */
+enum { DBSR_OUT_NHWC = 0, DBSR_OUT_SHUFFLE = 1, DBSR_OUT_NCHW_F32 = 2 };
+enum { DBSR_E_ARG = -1, DBSR_E_UNSUPPORTED = -2 };
+
+/* logical frame f -> stored image (f / fpg) * group_stride + group_offset + (f % fpg) * inner_stride.
+ * Identity: {1, 1, 0, 1}.  inner_stride 0 broadcasts one stored image to a group (e.g. every PWC
+ * pair of a burst reading that burst's reference frame). */
+typedef struct dbsr_frame_map {
+    int fpg;
+    int group_stride;
+    int group_offset;
+    int inner_stride;
+} dbsr_frame_map;
+
+typedef struct dbsr_tensor {          /* a channel slice of a batch of NHWC images */
+    void* ptr;
+    int dtype;                        /* DBSR_F32 / DBSR_BF16 */
+    long long img_stride;             /* elements between stored images */
+    int ld;                           /* elements between pixels */
+    int c0;                           /* first channel */
+    dbsr_frame_map map;
+} dbsr_tensor;
+
+/* Implicit-GEMM convolution on MFMA.  out = post_act(act(conv(x) + bias) + residual).
+ * Weights must be packed by dbsr_conv_pack_weights (dtype = x.dtype).
+ * out_mode DBSR_OUT_SHUFFLE writes PixelShuffle(shuffle) of the result (the packed weights must have
+ * been packed with the same shuffle factor); DBSR_OUT_NCHW_F32 writes an fp32 NCHW tensor
+ * (y.img_stride = Cout*out_h*out_w, ld/c0 ignored). */
+typedef struct dbsr_conv_desc {
+    int n_frames;
+    dbsr_tensor x;  int in_h, in_w, cin;
+    const void* w;  const float* bias;  int cout, kh, kw, stride, pad, dil;
+    dbsr_tensor y;  int out_h, out_w;
+    int act;
+    dbsr_tensor res;                  /* res.ptr == NULL: no residual */
+    int post_act;
+    int out_mode, shuffle;
+} dbsr_conv_desc;
+
+/* Packed weight layout: [cout_pad][kgp*8] with k-group kg = (ky*kw+kx)*(cin8/8) + c/8, where
+ * cin8 = round_up(cin, 8), kgp = round_up(kh*kw*cin8/8, 4), cout_pad = round_up(cout, 64). */
+size_t dbsr_conv_packed_elems(int cout, int cin, int kh, int kw);
+/* w_f32: torch layout [cout][cin][kh][kw] fp32 (device).  bias_f32 may be NULL.  With shuffle > 1
+ * the output channels are permuted for the DBSR_OUT_SHUFFLE epilogue (and bias_out likewise). */
+int dbsr_conv_pack_weights(const float* w_f32, const float* bias_f32, int cout, int cin, int kh, int kw,
+                           int dtype, int shuffle, void* w_packed, float* bias_out, void* stream);
+int dbsr_conv2d(const dbsr_conv_desc* d, void* stream);
+
+/* 81-channel cost volume of (first, second) over displacements [-4,4]^2, divided by C, followed by
+ * LeakyReLU(0.1) when leaky != 0.  first/second/out: NHWC slices; out channel (dy+4)*9+(dx+4). */
+int dbsr_correlation(int n_pairs, int h, int w, int c, dbsr_tensor first, dbsr_tensor second,
+                     dbsr_tensor out, int leaky, void* stream);
+
+/* PWC-Net backwarp of `in` (C channels) by flow*scale (flow: NHWC fp32 slice with 2 channels),
+ * bilinear, zero padding, validity mask (weight mass > 0.999). */
+int dbsr_backwarp(int n, int h, int w, int c, dbsr_tensor in, dbsr_tensor flow, float scale,
+                  dbsr_tensor out, void* stream);
+
+/* DBSR warp: bilinear sample of feat at (x + fx, y + fy), zero padding.  flow: fp32 NCHW
+ * [n][2][h][w] (the `offsets` tensor), flow_img_stride elements per image. */
+int dbsr_warp_bilinear(int n, int h, int w, int c, dbsr_tensor feat, const float* flow,
+                       long long flow_img_stride, dbsr_tensor out, void* stream);
+
+/* Softmax over the burst of logits[b,n] and weighted sum of feats[b,n].  Frame (b,n): logits image
+ * b*N+n; feature image: n==0 -> ref (map applied to b), n>0 -> oth (map applied to b*(N-1)+n-1).
+ * weights (optional, ptr NULL to skip): NHWC images b*N+n.  fused: NHWC images b. */
+int dbsr_fuse_softmax(int B, int N, int hw, int c, dbsr_tensor logits, dbsr_tensor ref, dbsr_tensor oth,
+                      dbsr_tensor fused, dbsr_tensor weights, void* stream);
+
+/* ConvTranspose2d(cin -> cout<=4, k=4, s=2, p=1): in NHWC slice [n][h][w], out NHWC fp32 [n][2h][2w].
+ * w: torch layout [cin][cout][4][4] fp32; bias [cout] fp32. */
+int dbsr_conv_transpose_k4s2(int n, int h, int w, int cin, int cout, dbsr_tensor in, const float* wgt,
+                             const float* bias, dbsr_tensor out, void* stream);
+
+/* burst [B][N][4][H][W] fp32 (NCHW frames) -> raw: NHWC 4-channel slice (frames b*N+n);
+ * rgb: NHWC 3-channel slice [B*N][Hp][Wp] = bilinear(align_corners=False) resize of (R,(G1+G2)/2,B). */
+int dbsr_pack_burst(int B, int N, int H, int W, const float* burst, dbsr_tensor raw, int Hp, int Wp,
+                    dbsr_tensor rgb, void* stream);
+
+/* flow: NHWC fp32 2-ch slice [P][hf][wf] (P = B*(N-1) pairs).  offsets: fp32 NCHW [P][2][H][W] =
+ * 20*bilinear(flow -> H x W) * (W/Wp, H/Hp).  offs_mod (optional): NHWC 2-ch slice, images b*N+n,
+ * = offsets % modulo with zeros for n == 0 (merging.py:98-105). */
+int dbsr_flow_finalize(int B, int N, int hf, int wf, dbsr_tensor flow, int H, int W, int Hp, int Wp,
+                       float* offsets, float modulo, dbsr_tensor offs_mod, void* stream);
+
+/* Depthwise 3x3 filter with zero padding on an NHWC slice of C channels. k: 9 floats (host). */
+int dbsr_gauss_blur3(int n, int h, int w, int c, dbsr_tensor in, const float* k_host, dbsr_tensor out,
+                     void* stream);
+
+/* proj: NHWC images b*N+n (C channels).  out: [base = proj[b,0] | diff = proj[b,n]-proj[b,0]]
+ * written at out.c0 .. out.c0+2C. */
+int dbsr_merge_prep(int B, int N, int hw, int c, dbsr_tensor proj, dbsr_tensor out, void* stream);
+
+/* cat([vol(81, already in place), first(C), flow(2), feat(2)]) for PWC decoder level inputs:
+ * writes first/flow/feat into out channels [c0+81, c0+81+C+4). first: map pair->ref frame. */
+int dbsr_pwc_assemble(int n_pairs, int h, int w, int c, dbsr_tensor first, dbsr_tensor flow,
+                      dbsr_tensor feat, dbsr_tensor out, void* stream);
+
+/* Fill an NHWC slice with zeros (used for channel padding of persistent buffers). */
+int dbsr_zero(void* ptr, size_t bytes, void* stream);
+
+const char* dbsr_last_error(void);
+int dbsr_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,87 @@
+"""CPU-only checks of the C ABI: the library loads, exports every function include/dbsr_hip.h
+declares, and rejects bad arguments with an error code + message (no GPU work is launched)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, 'include', 'dbsr_hip.h')
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r'/\*.*?\*/', '', src, flags=re.S)
+    return sorted(set(re.findall(r'\b(dbsr_[a-z0-9_]+)\s*\(', src)))
+
+
+@pytest.fixture(scope='module')
+def L():
+    from dbsr_amd import _lib
+    _lib.lib()
+    return _lib
+
+
+def test_header_declares_expected(L):
+    assert declared_functions() == sorted(L.EXPORTED)
+
+
+def test_library_exports_all_declared(L):
+    raw = ctypes.CDLL(L.LIB_PATH)
+    for name in declared_functions():
+        assert hasattr(raw, name), name
+    assert L.lib().dbsr_abi_version() == L.ABI_VERSION
+
+
+def test_struct_layout_matches_c():
+    from dbsr_amd import _lib
+    # dbsr_frame_map 16 B; dbsr_tensor: ptr 8, dtype 4 (+4 pad), img_stride 8, ld 4, c0 4, map 16 -> 48
+    assert ctypes.sizeof(_lib.FrameMap) == 16
+    assert ctypes.sizeof(_lib.Tensor) == 48
+
+
+def test_packed_size(L):
+    # cin 117 -> 120 (15 groups of 8) * 9 taps = 135 -> 136 k-groups; cout 128 -> 128 rows
+    assert L.lib().dbsr_conv_packed_elems(128, 117, 3, 3) == 128 * 136 * 8
+    assert L.lib().dbsr_conv_packed_elems(3, 32, 1, 1) == 64 * 4 * 8
+
+
+def test_conv_rejects_bad_desc(L):
+    lib = L.lib()
+    assert lib.dbsr_conv2d(None, None) == -1
+    assert b'null desc' in lib.dbsr_last_error()
+    d = L.ConvDesc()
+    d.n_frames = 1
+    d.x = L.Tensor(1234, L.DBSR_F32, 100, 12, 0, L.FrameMap(1, 1, 0, 1))     # ld not a multiple of 8
+    d.in_h = d.in_w = 4
+    d.cin, d.cout, d.kh, d.kw, d.stride, d.pad, d.dil = 4, 8, 3, 3, 1, 1, 1
+    d.w = 5678
+    d.y = L.Tensor(4321, L.DBSR_F32, 100, 8, 0, L.FrameMap(1, 1, 0, 1))
+    d.out_h = d.out_w = 4
+    assert lib.dbsr_conv2d(d, None) == -1
+    assert b'multiples of 8' in lib.dbsr_last_error()
+    d.x.ld = 8
+    d.out_h = 5                                                            # inconsistent geometry
+    assert lib.dbsr_conv2d(d, None) == -1
+    assert b'inconsistent' in lib.dbsr_last_error()
+
+
+def test_other_ops_reject_null(L):
+    lib = L.lib()
+    nt = L.NULL_TENSOR
+    assert lib.dbsr_correlation(1, 2, 2, 4, nt, nt, nt, 1, None) == -1
+    assert lib.dbsr_warp_bilinear(1, 2, 2, 8, nt, None, 0, nt, None) == -1
+    assert lib.dbsr_fuse_softmax(1, 2, 4, 8, nt, nt, nt, nt, nt, None) == -1
+    assert lib.dbsr_backwarp(1, 2, 2, 4, nt, nt, 1.0, nt, None) == -1
+
+
+def test_product_refuses_cpu_tensors():
+    import torch
+    import dbsr_amd
+    from dbsr_amd import ops
+    net = dbsr_amd.dbsrnet_cvpr2021(**dbsr_amd.DBSR_SYNTHETIC_KWARGS)
+    with pytest.raises(RuntimeError):
+        net(torch.zeros(1, 3, 4, 48, 48))
+    with pytest.raises(NotImplementedError):
+        ops.FunctionCorrelation(torch.zeros(1, 8, 4, 4), torch.zeros(1, 8, 4, 4))

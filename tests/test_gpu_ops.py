@@ -1,0 +1,125 @@
+"""Op-level parity of the HIP kernels (through the C ABI) against the oracle and the reference
+fixtures.  fp32 tolerances are written per test; bf16 tests use relative tolerances sized for
+8-bit mantissas with fp32 accumulation."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import dbsr_oracle as orc
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+@pytest.fixture(scope='module')
+def ops():
+    from dbsr_amd import ops as O
+    return O
+
+
+def test_correlation_fixture(golden, ops):
+    g = golden('ops')
+    out = ops.FunctionCorrelation(torch.from_numpy(g['corr_f1']).to(DEV), torch.from_numpy(g['corr_f2']).to(DEV))
+    np.testing.assert_allclose(out.cpu().numpy(), g['corr_out'], atol=1e-5, rtol=0)
+
+
+@pytest.mark.parametrize('shape', [(3, 196, 1, 1), (2, 128, 2, 2), (2, 96, 4, 4), (2, 64, 8, 8), (3, 32, 16, 16),
+                                   (1, 20, 5, 7)])
+def test_correlation_levels(ops, shape):
+    gen = torch.Generator().manual_seed(shape[1])
+    a, b = torch.randn(*shape, generator=gen), torch.randn(*shape, generator=gen)
+    out = ops.FunctionCorrelation(a.to(DEV), b.to(DEV), leaky=True)
+    ref = F.leaky_relu(orc.correlation(a, b), 0.1)
+    np.testing.assert_allclose(out.cpu().numpy(), ref.numpy(), atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize('tag', ['bw8', 'bw2'])
+def test_backwarp_fixture(golden, ops, tag):
+    g = golden('ops')
+    x = torch.from_numpy(g[f'{tag}_x']).to(DEV)
+    fl = torch.from_numpy(g[f'{tag}_flow']).to(DEV) * float(g[f'{tag}_scale'])
+    out = ops.backwarp(x, fl)
+    np.testing.assert_allclose(out.cpu().numpy(), g[f'{tag}_out'], atol=1e-5, rtol=0)
+
+
+def test_warp_fixture(golden, ops):
+    g = golden('ops')
+    out = ops.warp(torch.from_numpy(g['warp_x']).to(DEV), torch.from_numpy(g['warp_flow']).to(DEV))
+    np.testing.assert_allclose(out.cpu().numpy(), g['warp_out'], atol=1e-5, rtol=0)
+
+
+def test_warp_large_flow_and_zero(ops):
+    gen = torch.Generator().manual_seed(7)
+    x = torch.randn(4, 512, 48, 48, generator=gen)
+    fl = torch.randn(4, 2, 48, 48, generator=gen) * 4.0
+    fl[0] = 0.0
+    fl[3] *= 20.0             # mostly outside the frame -> zeros
+    out = ops.warp(x.to(DEV), fl.to(DEV)).cpu()
+    np.testing.assert_allclose(out.numpy(), orc.warp(x, fl).numpy(), atol=1e-5, rtol=0)
+
+
+CONV_CASES = [
+    # (N, Cin, H, W, Cout, k, stride, pad, dil)
+    (3, 4, 12, 12, 64, 3, 1, 1, 1),
+    (2, 64, 16, 16, 64, 3, 1, 1, 1),
+    (2, 64, 9, 11, 512, 3, 1, 1, 1),
+    (2, 512, 7, 7, 64, 1, 1, 0, 1),
+    (2, 3, 64, 64, 16, 3, 2, 1, 1),
+    (3, 196, 1, 1, 128, 3, 1, 1, 1),
+    (2, 117, 16, 16, 128, 3, 1, 1, 1),
+    (2, 565, 16, 16, 128, 3, 1, 1, 1),
+    (2, 128, 16, 16, 96, 3, 1, 8, 8),
+    (2, 64, 16, 16, 32, 3, 1, 16, 16),
+    (2, 32, 16, 16, 2, 3, 1, 1, 1),
+    (2, 2, 10, 10, 64, 3, 1, 1, 1),
+    (1, 32, 40, 24, 3, 1, 1, 0, 1),
+]
+
+
+@pytest.mark.parametrize('case', CONV_CASES)
+def test_conv2d_fp32(ops, case):
+    N, Cin, H, W, Cout, k, s, p, d = case
+    gen = torch.Generator().manual_seed(Cin * 1000 + Cout)
+    x = torch.randn(N, Cin, H, W, generator=gen)
+    w = torch.randn(Cout, Cin, k, k, generator=gen) / (Cin * k * k) ** 0.5
+    b = torch.randn(Cout, generator=gen) * 0.1
+    ref = F.leaky_relu(F.conv2d(x, w, b, stride=s, padding=p, dilation=d), 0.1)
+    out = ops.conv2d(x.to(DEV), w.to(DEV), b.to(DEV), stride=s, padding=p, dilation=d, act=2).cpu()
+    np.testing.assert_allclose(out.numpy(), ref.numpy(), atol=2e-5, rtol=1e-4)
+
+
+@pytest.mark.parametrize('case', CONV_CASES[:4])
+def test_conv2d_bf16(ops, case):
+    N, Cin, H, W, Cout, k, s, p, d = case
+    gen = torch.Generator().manual_seed(Cin * 1000 + Cout + 1)
+    x = torch.randn(N, Cin, H, W, generator=gen)
+    w = torch.randn(Cout, Cin, k, k, generator=gen) / (Cin * k * k) ** 0.5
+    xb = x.to(torch.bfloat16).float()
+    wb = w.to(torch.bfloat16).float()
+    ref = F.conv2d(xb, wb, None, stride=s, padding=p, dilation=d)    # same rounded inputs, fp32 math
+    out = ops.conv2d(x.to(DEV), w.to(DEV), None, stride=s, padding=p, dilation=d,
+                     compute_dtype=torch.bfloat16, out_f32=True).cpu()
+    np.testing.assert_allclose(out.numpy(), ref.numpy(), atol=1e-4, rtol=1e-4)
+
+
+def test_conv2d_residual_relu(ops):
+    gen = torch.Generator().manual_seed(5)
+    x = torch.randn(2, 64, 12, 12, generator=gen)
+    w = torch.randn(64, 64, 3, 3, generator=gen) / 24.0
+    b = torch.randn(64, generator=gen) * 0.1
+    res = torch.randn(2, 64, 12, 12, generator=gen)
+    ref = F.relu(F.conv2d(x, w, b, padding=1) + res)
+    out = ops.conv2d(x.to(DEV), w.to(DEV), b.to(DEV), padding=1, residual=res.to(DEV), post_act=1).cpu()
+    np.testing.assert_allclose(out.numpy(), ref.numpy(), atol=2e-5, rtol=1e-4)
+
+
+def test_pwcnet_fixture(golden, synth_sd):
+    import dbsr_amd
+    g = golden('ops')
+    net = dbsr_amd.dbsrnet_cvpr2021(**dbsr_amd.DBSR_SYNTHETIC_KWARGS)
+    net.load_state_dict(synth_sd)
+    pwc = net.encoder.alignment_net.to(DEV)
+    with torch.no_grad():
+        fl = pwc(torch.from_numpy(g['pwc_src']).to(DEV), torch.from_numpy(g['pwc_tgt']).to(DEV))
+    np.testing.assert_allclose(fl.cpu().numpy(), g['pwc_flow'], atol=1e-3, rtol=0)
