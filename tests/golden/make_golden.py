@@ -97,6 +97,10 @@ def main():
         if zf:
             ref_net.encoder.alignment_net.forward = saved
         fw = aux['fusion_weights']
+        # ground truth stored as uint16 (/65535): torch's CPU randn differs across CPU ISAs, so the
+        # GPU box cannot regenerate it bit-identically
+        gt_u16 = (gt.clamp(0, 1) * 65535).round().to(torch.int32).numpy().astype(np.uint16)
+        gt = torch.from_numpy(gt_u16.astype(np.float32)) / 65535.0
         psnr = [float(10 * torch.log10(1.0 / ((p - q)[..., 40:-40, 40:-40] ** 2).mean()))
                 for p, q in zip(quantize_f(pred), gt)]           # image_quality_v2.py:69-101, bi=40
         d = dict(burst=burst.numpy(), seed=np.int64(seed), ref_psnr=np.array(psnr, dtype=np.float64),
@@ -107,6 +111,8 @@ def main():
                  fw_crop=fw[:, :, :16, 8:16, 8:16].numpy(),
                  pred_sum=pred.double().sum(dim=(-2, -1)).float().numpy(),
                  zero_flow=np.array(zf))
+        if name in ('e2e_b1n14', 'e2e_b1n4'):
+            d['gt_u16'] = gt_u16
         if name == 'e2e_b1n14':
             d['pred_q'] = quantize(pred)
         out[name] = d
