@@ -22,6 +22,13 @@ using namespace dbsr;
 
 namespace {
 
+inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
+// channel padding of the packed K dimension (dbsr_hip.h): 8 for cin <= 16, else 32, so every
+// conv with cin > 16 is a whole number of 32-channel MFMA chunks per tap
+inline int cin_pad(int cin) { return cin <= 16 ? round_up(cin, 8) : round_up(cin, 32); }
+
+int g_tiled_enabled = 1;   // dbsr_set_conv_algo(0) forces the generic kernel (A/B testing)
+
 struct ConvK {
     const void* x; long long x_is; int x_ld; dbsr_frame_map xm; int in_h, in_w;
     const void* w; const float* bias; int Kp, KG, KGp, CG, kw, stride, pad, dil, cout;
@@ -123,14 +130,13 @@ __global__ __launch_bounds__(256) void conv2d_kernel(ConvK k) {
 #pragma unroll
         for (int j = 0; j < NT; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-    // k-group decode for this lane, advanced incrementally by 4 per k-step
+    // k-group decode of the next k-step to load, advanced incrementally by 4 per k-step
     int tap = kgl / k.CG;
     int cg = kgl - tap * k.CG;
     int ky = tap / k.kw, kx = tap - (tap / k.kw) * k.kw;
     const int nks = k.KGp >> 2;
-    for (int ks = 0; ks < nks; ++ks) {
+    auto load = [&](int ks, Frag<T> (&a)[MT], Frag<T> (&b)[NT]) {
         const bool kval = ks * 4 + kgl < k.KG;
-        Frag<T> a[MT], b[NT];
 #pragma unroll
         for (int i = 0; i < MT; ++i) a[i].load(wr[i] + ks * 32);
         const int dy = ky * k.dil, dx = kx * k.dil;
@@ -142,14 +148,37 @@ __global__ __launch_bounds__(256) void conv2d_kernel(ConvK k) {
             else
                 b[j].zero();
         }
-#pragma unroll
-        for (int i = 0; i < MT; ++i)
-#pragma unroll
-            for (int j = 0; j < NT; ++j) acc[i][j] = mma(a[i], b[j], acc[i][j]);
         cg += 4;
         while (cg >= k.CG) {
             cg -= k.CG;
             if (++kx == k.kw) { kx = 0; ++ky; }
+        }
+    };
+    auto compute = [&](const Frag<T> (&a)[MT], const Frag<T> (&b)[NT]) {
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int j = 0; j < NT; ++j) acc[i][j] = mma(a[i], b[j], acc[i][j]);
+    };
+    if constexpr (sizeof(T) == 2) {
+        // one k-step of register prefetch: the loads of step s+1 are in flight during step s's MFMAs
+        Frag<T> a0[MT], b0[NT], a1[MT], b1[NT];
+        load(0, a0, b0);
+        int ks = 0;
+        for (; ks + 1 < nks; ks += 2) {
+            load(ks + 1, a1, b1);
+            compute(a0, b0);
+            if (ks + 2 < nks) load(ks + 2, a0, b0);
+            compute(a1, b1);
+        }
+        if (ks < nks) compute(a0, b0);
+    } else {
+        // fp32 (parity mode): fragments are twice as wide; no prefetch (the prefetched variant also
+        // trips a ROCm 7.2 machine-copy-propagation crash)
+        for (int ks = 0; ks < nks; ++ks) {
+            Frag<T> a0[MT], b0[NT];
+            load(ks, a0, b0);
+            compute(a0, b0);
         }
     }
 
@@ -227,6 +256,196 @@ __global__ void pack_weights_kernel(const float* __restrict__ w, const float* __
     if (bias_out && kk == 0 && co < cout) bias_out[co] = bias ? bias[co_src] : 0.f;
 }
 
+// ------------------------------------------------------------------------------------------------
+// LDS-tiled 3x3 / stride 1 / pad 1 convolution for Cin % 32 == 0 (the ResNet trunks: encoder,
+// weight predictor, decoder; ~2/3 of the forward's FLOPs).
+//
+// Block = 4 waves = WM output channels x a spatial tile of TH x 16 pixels of one frame (each wave
+// owns WN = 4*16*(TH/4) ... i.e. TH/4 rows of 16 pixels).  Per 32-channel input chunk the block
+// stages into LDS (a) the (TH+2) x 18 halo tile and (b) the chunk's weights for all 9 taps, then
+// every wave runs 9 taps x (WM/16) x (WN/16) MFMAs reading both operands with ds_read_b128.
+// The next chunk's global loads are issued into registers before the current chunk's MFMAs and
+// written to LDS after them (async-stage split), with one LDS buffer and two barriers per chunk
+// (two blocks per CU overlap each other's barriers).
+//
+// LDS images are [k-group plane][row][16 B] with each plane a multiple of 256 B: any 16
+// consecutive pixels (or output channels) of one plane then cover all 64 banks, for every tap
+// shift, under ds_read_b128's lane groups ({0-3,12-15,20-27}, ...), because lane l reads row
+// (l&15) of plane (l>>4) -- conflict-free by construction (conv tiling).
+// Blocks are ordered so each XCD gets a contiguous range of (tile, cout-tile) pairs: the 8 cout
+// tiles of a spatial tile and neighbouring tiles (shared halos) hit the same L2.
+// ------------------------------------------------------------------------------------------------
+template <typename T, int WM, int WN>
+struct TileCfg {
+    static constexpr int TW = 16, TH = 4 * WN / 16, HWD = TW + 2, HHT = TH + 2;
+    static constexpr int NQ = HHT * HWD;
+    static constexpr int HALVES = sizeof(T) / 2;              // 16-B halves per k-group (bf16 1, f32 2)
+    static constexpr int IN_ITEMS = (NQ + 15) / 16 * HALVES;  // 1-KiB LDS pieces: (16-pixel block, half)
+    static constexpr int W_ITEMS = 9 * (WM / 16) * HALVES;    // 1-KiB LDS pieces: (tap, 16-cout block, half)
+    static constexpr int IN_U4 = IN_ITEMS * 64, W_U4 = W_ITEMS * 64;
+};
+
+// 16 zero bytes per lane for halo pixels outside the frame (LDS-DMA cannot write zeros itself)
+__device__ __attribute__((aligned(16))) u32x4_t g_dbsr_zero16[64];
+
+__device__ __forceinline__ void glds16(const void* src, u32x4_t* lds_piece) {
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_piece, 16, 0, 0);
+}
+
+template <typename T, int WM, int WN>
+__global__ __launch_bounds__(256, 2) void conv3x3_tiled_kernel(ConvK k, int tiles_x, int tiles_y, int nct,
+                                                               int nblocks) {
+    using C = TileCfg<T, WM, WN>;
+    // One LDS array (a second __shared__ object can de-pipeline LDS-DMA: cdna_hip_programming.md §5 item 4a)
+    __shared__ __attribute__((aligned(16))) u32x4_t lds[C::IN_U4 + C::W_U4];
+    u32x4_t* lin = lds;                 // [pixel block][half][g][16 px] x 16 B
+    u32x4_t* lw = lds + C::IN_U4;       // [tap][cout block][half][g][16 co] x 16 B
+
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int g = lane >> 4, col = lane & 15;
+
+    // XCD-grouped block order (bijective; cdna_hip_programming.md §5 'XCD swizzle')
+    const int bid = blockIdx.x;
+    const int xcd = bid & 7, q8 = nblocks >> 3, r8 = nblocks & 7;
+    const int lin_id = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    const int ct = lin_id % nct;
+    int tile = lin_id / nct;
+    const int tx = tile % tiles_x; tile /= tiles_x;
+    const int ty = tile % tiles_y;
+    const int f = tile / tiles_y;
+    const int y0 = ty * C::TH, x0 = tx * C::TW;
+    const int c_base = ct * WM;
+
+    const T* xf = (const T*)k.x + map_frame(k.xm, f) * k.x_is;
+    const int nchunks = k.CG / 4;
+
+    // Stage one 32-channel chunk: every wave-instruction moves one 1-KiB piece, lane l -> (k-group l>>4,
+    // pixel/cout l&15), so the LDS image is lane-linear (LDS-DMA) and 16 consecutive rows of a plane
+    // occupy 16 distinct 16-B bank slots (conflict-free ds_read_b128 for any tap shift).
+    auto issue = [&](int chunk) {
+        for (int item = wave; item < C::IN_ITEMS; item += 4) {
+            const int qb = item / C::HALVES, h = item % C::HALVES;
+            const int q = qb * 16 + col;
+            const void* src = g_dbsr_zero16;
+            if (q < C::NQ) {
+                const int iy = y0 - 1 + q / C::HWD, ix = x0 - 1 + q % C::HWD;
+                if ((unsigned)iy < (unsigned)k.in_h && (unsigned)ix < (unsigned)k.in_w)
+                    src = xf + ((long long)iy * k.in_w + ix) * k.x_ld + chunk * 32 + g * 8 + h * 4;
+            }
+            glds16(src, lin + item * 64);
+        }
+        for (int item = wave; item < C::W_ITEMS; item += 4) {
+            const int h = item % C::HALVES, rest = item / C::HALVES;
+            const int cb = rest % (WM / 16), tap = rest / (WM / 16);
+            const int co = c_base + cb * 16 + col;
+            glds16((const T*)k.w + (long long)co * k.Kp + (tap * k.CG + chunk * 4 + g) * 8 + h * 4, lw + item * 64);
+        }
+    };
+
+    f32x4_t acc[WM / 16][WN / 16];
+#pragma unroll
+    for (int i = 0; i < WM / 16; ++i)
+#pragma unroll
+        for (int j = 0; j < WN / 16; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    const int row0 = wave * (WN / 16);
+    for (int chunk = 0; chunk < nchunks; ++chunk) {
+        issue(chunk);
+        __syncthreads();                 // vmcnt(0) for the LDS-DMA + barrier
+#pragma unroll 3
+        for (int tap = 0; tap < 9; ++tap) {
+            const int ky = tap / 3, kx = tap % 3;
+            Frag<T> a[WM / 16], b[WN / 16];
+#pragma unroll
+            for (int i = 0; i < WM / 16; ++i) {
+                const u32x4_t* p = lw + ((tap * (WM / 16) + i) * C::HALVES) * 64 + g * 16 + col;
+                if constexpr (sizeof(T) == 2) {
+                    a[i].v = __builtin_bit_cast(bf16x8_t, p[0]);
+                } else {
+                    a[i].a = __builtin_bit_cast(float4, p[0]);
+                    a[i].b = __builtin_bit_cast(float4, p[64]);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < WN / 16; ++j) {
+                const int q = (row0 + j + ky) * C::HWD + kx + col;
+                const u32x4_t* p = lin + ((q >> 4) * C::HALVES) * 64 + g * 16 + (q & 15);
+                if constexpr (sizeof(T) == 2) {
+                    b[j].v = __builtin_bit_cast(bf16x8_t, p[0]);
+                } else {
+                    b[j].a = __builtin_bit_cast(float4, p[0]);
+                    b[j].b = __builtin_bit_cast(float4, p[64]);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < WM / 16; ++i)
+#pragma unroll
+                for (int j = 0; j < WN / 16; ++j) acc[i][j] = mma(a[i], b[j], acc[i][j]);
+        }
+        __syncthreads();                 // all waves done reading before the next chunk lands
+    }
+
+    // ---- epilogue ----
+#pragma unroll
+    for (int j = 0; j < WN / 16; ++j) {
+        const int oy = y0 + row0 + j, ox = x0 + col;
+        if (oy >= k.out_h || ox >= k.out_w) continue;
+        const int rr = oy * k.out_w + ox;
+#pragma unroll
+        for (int i = 0; i < WM / 16; ++i) {
+            const int co = c_base + i * 16 + g * 4;
+            if (co >= k.cout) continue;
+            const int nvalid = min(4, k.cout - co);
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float t = acc[i][j][r];
+                if (k.bias && r < nvalid) t += k.bias[co + r];
+                v[r] = apply_act(t, k.act);
+            }
+            if (k.r) {
+                const long long roff = map_frame(k.rm, f) * k.r_is + (long long)rr * k.r_ld + k.r_c0 + co;
+                float rv[4] = {0.f, 0.f, 0.f, 0.f};
+                if (nvalid == 4 && k.vec_store) {
+                    if (k.y_f32) {
+                        float4 q = *(const float4*)((const float*)k.r + roff);
+                        rv[0] = q.x; rv[1] = q.y; rv[2] = q.z; rv[3] = q.w;
+                    } else if constexpr (sizeof(T) == 2) {
+                        uint2 q = *(const uint2*)((const T*)k.r + roff);
+                        rv[0] = __uint_as_float(q.x << 16); rv[1] = __uint_as_float(q.x & 0xffff0000u);
+                        rv[2] = __uint_as_float(q.y << 16); rv[3] = __uint_as_float(q.y & 0xffff0000u);
+                    } else {
+                        float4 q = *(const float4*)((const T*)k.r + roff);
+                        rv[0] = q.x; rv[1] = q.y; rv[2] = q.z; rv[3] = q.w;
+                    }
+                } else {
+                    for (int r = 0; r < nvalid; ++r)
+                        rv[r] = k.y_f32 ? ((const float*)k.r)[roff + r] : elem<T>::ld((const T*)k.r + roff + r);
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = apply_act(v[r] + rv[r], k.post_act);
+            }
+            store4<T>(k, map_frame(k.ym, f) * k.y_is + (long long)rr * k.y_ld + k.y_c0 + co, v, nvalid);
+        }
+    }
+}
+
+template <typename T, int WM, int WN>
+int launch_tiled(const ConvK& k, int n_frames, hipStream_t s) {
+    using C = TileCfg<T, WM, WN>;
+    const int tiles_x = (k.out_w + C::TW - 1) / C::TW, tiles_y = (k.out_h + C::TH - 1) / C::TH;
+    const int nct = (k.cout + WM - 1) / WM;
+    const long long nb = (long long)n_frames * tiles_x * tiles_y * nct;
+    if (nb >= (1LL << 31)) {
+        dbsr_set_error("conv2d: grid too large");
+        return DBSR_E_ARG;
+    }
+    hipLaunchKernelGGL((conv3x3_tiled_kernel<T, WM, WN>), dim3((unsigned)nb), dim3(256), 0, s, k, tiles_x, tiles_y,
+                       nct, (int)nb);
+    DBSR_LAUNCH_CHECK();
+    return 0;
+}
+
 template <typename T, int MT, int NT>
 int launch_conv(const ConvK& k, hipStream_t s) {
     dim3 grid((k.npix + 4 * NT * 16 - 1) / (4 * NT * 16), (k.cout + MT * 16 - 1) / (MT * 16));
@@ -236,21 +455,45 @@ int launch_conv(const ConvK& k, hipStream_t s) {
 }
 
 template <typename T>
-int dispatch_conv(const ConvK& k, hipStream_t s) {
-    const int tiles4 = (k.npix + 255) / 256;
-    const bool small = tiles4 * ((k.cout + 63) / 64) < 512;   // too few blocks to fill 256 CUs
-    if (k.cout <= 16) return small ? launch_conv<T, 1, 2>(k, s) : launch_conv<T, 1, 4>(k, s);
-    if (k.cout <= 32) return small ? launch_conv<T, 2, 2>(k, s) : launch_conv<T, 2, 4>(k, s);
-    return small ? launch_conv<T, 4, 2>(k, s) : launch_conv<T, 4, 4>(k, s);
+int dispatch_conv(const ConvK& k, const dbsr_conv_desc* d, hipStream_t s) {
+    const bool tiled_ok = d->kh == 3 && d->kw == 3 && d->stride == 1 && d->pad == 1 && d->dil == 1 &&
+                          d->cin > 16 && d->out_h >= 8 && d->out_w >= 8 && d->out_mode == DBSR_OUT_NHWC &&
+                          g_tiled_enabled;
+    if (tiled_ok) {
+        if (k.cout <= 32) return launch_tiled<T, 32, 128>(k, d->n_frames, s);
+        return launch_tiled<T, 64, 64>(k, d->n_frames, s);
+    }
+    // generic kernel: the largest tile that still gives >= 2 blocks per CU (512 blocks); tiny PWC levels
+    // (a few hundred pixels) fall through to 16 x 64-pixel tiles for parallelism
+    const int mts[3] = {4, 2, 1}, nts[3] = {4, 2, 1};
+    int best_m = 1, best_n = 1;
+    bool found = false;
+    for (int a = 0; a < 3 && !found; ++a) {
+        if (mts[a] > 1 && k.cout <= (mts[a] / 2) * 16) continue;          // do not pad cout beyond need
+        for (int b = 0; b < 3 && !found; ++b) {
+            const long long blocks = (long long)((k.npix + 64 * nts[b] - 1) / (64 * nts[b])) *
+                                     ((k.cout + 16 * mts[a] - 1) / (16 * mts[a]));
+            if (blocks >= 512) { best_m = mts[a]; best_n = nts[b]; found = true; }
+        }
+    }
+    if (!found) { best_m = 1; best_n = 1; }
+#define DBSR_CONV_CASE(M, N) if (best_m == M && best_n == N) return launch_conv<T, M, N>(k, s);
+    DBSR_CONV_CASE(4, 4) DBSR_CONV_CASE(4, 2) DBSR_CONV_CASE(4, 1)
+    DBSR_CONV_CASE(2, 4) DBSR_CONV_CASE(2, 2) DBSR_CONV_CASE(2, 1)
+    DBSR_CONV_CASE(1, 4) DBSR_CONV_CASE(1, 2) DBSR_CONV_CASE(1, 1)
+#undef DBSR_CONV_CASE
+    return launch_conv<T, 1, 1>(k, s);
 }
-
-inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
 
 }  // namespace
 
+extern "C" int dbsr_set_conv_algo(int tiled) {
+    g_tiled_enabled = tiled ? 1 : 0;
+    return 0;
+}
+
 extern "C" size_t dbsr_conv_packed_elems(int cout, int cin, int kh, int kw) {
-    const int cin8 = round_up(cin, 8);
-    const int KGp = round_up(kh * kw * (cin8 / 8), 4);
+    const int KGp = round_up(kh * kw * (cin_pad(cin) / 8), 4);
     return (size_t)round_up(cout, 64) * KGp * 8;
 }
 
@@ -262,7 +505,7 @@ extern "C" int dbsr_conv_pack_weights(const float* w_f32, const float* bias_f32,
     if (shuffle > 1)
         DBSR_CHECK_ARG(cout % (shuffle * shuffle) == 0 && (cout / (shuffle * shuffle)) % 4 == 0,
                        "pack_weights: cout %d not divisible for shuffle %d", cout, shuffle);
-    const int CG = round_up(cin, 8) / 8, KG = kh * kw * CG, KGp = round_up(KG, 4), Kp = KGp * 8;
+    const int CG = cin_pad(cin) / 8, KG = kh * kw * CG, KGp = round_up(KG, 4), Kp = KGp * 8;
     const int cout_pad = round_up(cout, 64);
     const long long total = (long long)cout_pad * Kp;
     hipLaunchKernelGGL(pack_weights_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
@@ -281,7 +524,7 @@ extern "C" int dbsr_conv2d(const dbsr_conv_desc* d, void* stream) {
     DBSR_CHECK_ARG(d->cin > 0 && d->cout > 0 && d->kh > 0 && d->kw > 0 && d->stride > 0 && d->dil > 0, "conv2d: bad shape");
     DBSR_CHECK_ARG(d->x.ld % 8 == 0 && d->x.c0 % 8 == 0, "conv2d: input ld/c0 must be multiples of 8 (got %d/%d)",
                    d->x.ld, d->x.c0);
-    DBSR_CHECK_ARG(d->x.c0 + round_up(d->cin, 8) <= d->x.ld, "conv2d: input channel slice exceeds ld");
+    DBSR_CHECK_ARG(d->x.c0 + cin_pad(d->cin) <= d->x.ld, "conv2d: input slice [c0, c0+cin_pad) exceeds ld");
     DBSR_CHECK_ARG(d->x.map.fpg > 0 && d->y.map.fpg > 0, "conv2d: frame map fpg must be > 0");
     DBSR_CHECK_ARG(d->out_h == (d->in_h + 2 * d->pad - d->dil * (d->kh - 1) - 1) / d->stride + 1 &&
                    d->out_w == (d->in_w + 2 * d->pad - d->dil * (d->kw - 1) - 1) / d->stride + 1,
@@ -303,7 +546,7 @@ extern "C" int dbsr_conv2d(const dbsr_conv_desc* d, void* stream) {
     // the channel offset is folded into the base pointer (x.c0 is a multiple of 8)
     const int esz = d->x.dtype == DBSR_BF16 ? 2 : 4;
     k.x = (const char*)d->x.ptr + (long long)d->x.c0 * esz;
-    const int CG = round_up(d->cin, 8) / 8;
+    const int CG = cin_pad(d->cin) / 8;
     k.CG = CG; k.KG = d->kh * d->kw * CG; k.KGp = round_up(k.KG, 4); k.Kp = k.KGp * 8;
     k.w = d->w; k.bias = d->bias; k.kw = d->kw; k.stride = d->stride; k.pad = d->pad; k.dil = d->dil; k.cout = d->cout;
     k.y = d->y.ptr; k.y_f32 = d->y.dtype == DBSR_F32; k.y_is = d->y.img_stride; k.y_ld = d->y.ld; k.y_c0 = d->y.c0;
@@ -315,5 +558,5 @@ extern "C" int dbsr_conv2d(const dbsr_conv_desc* d, void* stream) {
     k.npix = (int)npix;
     k.vec_store = (d->out_mode != DBSR_OUT_NCHW_F32) && (d->y.ld % 4 == 0) && (d->y.c0 % 4 == 0);
     hipStream_t s = (hipStream_t)stream;
-    return d->x.dtype == DBSR_BF16 ? dispatch_conv<bf16_t>(k, s) : dispatch_conv<float>(k, s);
+    return d->x.dtype == DBSR_BF16 ? dispatch_conv<bf16_t>(k, d, s) : dispatch_conv<float>(k, d, s);
 }

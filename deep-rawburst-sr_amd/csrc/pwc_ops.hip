@@ -94,12 +94,13 @@ __global__ void backwarp_kernel(int n, int h, int w, int C, dbsr_tensor in, dbsr
 // ------------------------------------------------------------------------------------------------
 // ConvTranspose2d(k=4, s=2, p=1) (pwcnet.py:119-120): out[oy,ox,co] = b[co] + sum over the 2x2 input
 // pixels iy=(oy+1-ky)/2, ix=(ox+1-kx)/2 and all ci of in[iy,ix,ci]*w[ci,co,ky,kx].
-// One wave per output pixel, lanes stride over input channels, shuffle reduction.
+// Weights repacked as [ky][kx][co][cin8] (zero-padded to a multiple of 8 channels) so a wave reads
+// them contiguously; one wave per output pixel, lane = 8-channel group, shuffle reduction.
 // ------------------------------------------------------------------------------------------------
 template <typename T>
-__global__ __launch_bounds__(256) void convt_k4s2_kernel(int n, int h, int w, int cin, int cout, dbsr_tensor in,
+__global__ __launch_bounds__(256) void convt_k4s2_kernel(int n, int h, int w, int cin8, int cout, dbsr_tensor in,
                                                          const float* __restrict__ wgt, const float* __restrict__ bias,
-                                                         dbsr_tensor out) {
+                                                         dbsr_tensor out, int vec) {
     const int lane = threadIdx.x & 63;
     const long long opix = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int H2 = 2 * h, W2 = 2 * w;
@@ -110,6 +111,7 @@ __global__ __launch_bounds__(256) void convt_k4s2_kernel(int n, int h, int w, in
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
     const T* base = img_ptr<T>(in, p);
     const int ky0 = (oy + 1) & 1, kx0 = (ox + 1) & 1;
+    const int ngroups = cin8 / 8;
     for (int a = 0; a < 2; ++a) {
         const int ky = ky0 + 2 * a, iy = (oy + 1 - ky) >> 1;
         if (iy < 0 || iy >= h) continue;
@@ -117,12 +119,24 @@ __global__ __launch_bounds__(256) void convt_k4s2_kernel(int n, int h, int w, in
             const int kx = kx0 + 2 * bq, ix = (ox + 1 - kx) >> 1;
             if (ix < 0 || ix >= w) continue;
             const T* src = base + ((long long)iy * w + ix) * in.ld;
-            for (int ci = lane; ci < cin; ci += 64) {
-                const float v = elem<T>::ld(src + ci);
-                const float* wp = wgt + ((long long)ci * cout) * 16 + ky * 4 + kx;
+            const float* wt = wgt + (long long)((ky * 4 + kx) * cout) * cin8;
+            for (int cgi = lane; cgi < ngroups; cgi += 64) {
+                float v[8];
+                if (vec) {
+                    load8(src + cgi * 8, v);
+                } else {
 #pragma unroll
-                for (int co = 0; co < 4; ++co)
-                    if (co < cout) acc[co] = fmaf(v, wp[co * 16], acc[co]);
+                    for (int j = 0; j < 8; ++j) v[j] = elem<T>::ld(src + cgi * 8 + j);
+                }
+#pragma unroll
+                for (int co = 0; co < 4; ++co) {
+                    if (co < cout) {
+                        float wv[8];
+                        load8(wt + (long long)co * cin8 + cgi * 8, wv);
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) acc[co] = fmaf(v[j], wv[j], acc[co]);
+                    }
+                }
             }
         }
     }
@@ -316,11 +330,14 @@ extern "C" int dbsr_conv_transpose_k4s2(int n, int h, int w, int cin, int cout, 
                                         const float* bias, dbsr_tensor out, void* stream) {
     DBSR_CHECK_ARG(map_ok(in) && map_ok(out) && wgt, "conv_transpose: bad tensor");
     DBSR_CHECK_ARG(out.dtype == DBSR_F32 && cout >= 1 && cout <= 4 && cin > 0, "conv_transpose: out f32, cout<=4");
+    const int cin8 = (cin + 7) / 8 * 8;
+    DBSR_CHECK_ARG(in.c0 + cin8 <= in.ld, "conv_transpose: input slice [c0, c0+round_up(cin,8)) exceeds ld");
+    const int vec = in.ld % 8 == 0 && in.c0 % 8 == 0;
     const long long opix = (long long)n * 4 * h * w;
     return by_dtype(in.dtype, [&](auto* tag) {
         using T = std::remove_pointer_t<decltype(tag)>;
         hipLaunchKernelGGL(convt_k4s2_kernel<T>, dim3(nblocks(opix, 4)), dim3(256), 0, (hipStream_t)stream, n, h, w,
-                           cin, cout, in, wgt, bias, out);
+                           cin8, cout, in, wgt, bias, out, vec);
         DBSR_LAUNCH_CHECK();
         return 0;
     });

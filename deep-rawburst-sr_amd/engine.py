@@ -42,6 +42,21 @@ def r8(c):
     return (c + 7) // 8 * 8
 
 
+def cpad(c):
+    """Pixel stride for a tensor that convs read: dbsr_conv2d reads cin rounded up to 8 (cin <= 16)
+    or 32 (cin > 16) channels (dbsr_hip.h, packed weight layout)."""
+    return r8(c) if c <= 16 else (c + 31) // 32 * 32
+
+
+def pack_convt(mod, device):
+    """nn.ConvTranspose2d weight [cin][cout][4][4] -> [ky][kx][cout][cin8] fp32 (dbsr_conv_transpose_k4s2)."""
+    w = mod.weight.detach().to(device=device, dtype=torch.float32)
+    cin = w.shape[0]
+    w = w.permute(2, 3, 1, 0).contiguous()
+    w = torch.nn.functional.pad(w, (0, r8(cin) - cin)).contiguous()
+    return w, mod.bias.detach().to(device=device, dtype=torch.float32).contiguous()
+
+
 def gauss_kernel3(sd, ksz=3):
     """PixShuffleUpsampler._get_gaussian_kernel (upsampling.py:24-29) via gauss_2d (filtering.py:20-40)."""
     k = torch.arange(-(ksz - 1) / 2, (ksz + 1) / 2, dtype=torch.float32).reshape(1, -1)
@@ -170,10 +185,8 @@ class PWCPlanner:
             ent = {'dense': [W.conv(getattr(d, n)[0]) for n in ['netOne', 'netTwo', 'netThr', 'netFou', 'netFiv']],
                    'flow': W.conv(d.netSix[0])}
             if level < 6:
-                ent['upflow'] = (d.netUpflow.weight.detach().to(W.device, torch.float32).contiguous(),
-                                 d.netUpflow.bias.detach().to(W.device, torch.float32).contiguous())
-                ent['upfeat'] = (d.netUpfeat.weight.detach().to(W.device, torch.float32).contiguous(),
-                                 d.netUpfeat.bias.detach().to(W.device, torch.float32).contiguous())
+                ent['upflow'] = pack_convt(d.netUpflow, W.device)
+                ent['upfeat'] = pack_convt(d.netUpfeat, W.device)
             self.dec[level] = ent
         self.ref = [W.conv(net.netRefiner.netMain[i]) for i in range(0, 13, 2)]
 
@@ -188,9 +201,9 @@ class PWCPlanner:
         for k in range(6):
             C = PWC_LEVEL_CH[k + 1]
             oh, ow = self.ext[k][0].out_hw(*hw)
-            ta = NHWC(nF, oh, ow, r8(C), dtype, device)
-            tb = NHWC(nF, oh, ow, r8(C), dtype, device)
-            lv = NHWC(nF, oh, ow, r8(C), dtype, device)
+            ta = NHWC(nF, oh, ow, cpad(C), dtype, device)
+            tb = NHWC(nF, oh, ow, cpad(C), dtype, device)
+            lv = NHWC(nF, oh, ow, cpad(C), dtype, device)
             plan.conv(f'pwc.ext{k + 1}.0', self.ext[k][0], nF, x, 0, hw, ta, 0, L.ACT_LRELU)
             plan.conv(f'pwc.ext{k + 1}.2', self.ext[k][1], nF, ta, 0, (oh, ow), tb, 0, L.ACT_LRELU)
             plan.conv(f'pwc.ext{k + 1}.4', self.ext[k][2], nF, tb, 0, (oh, ow), lv, 0, L.ACT_LRELU)
@@ -203,14 +216,14 @@ class PWCPlanner:
             feat = levels[level]
             h, w, C = feat.h, feat.w, PWC_LEVEL_CH[level]
             base_real = 81 if level == 6 else 81 + C + 4
-            ld = BASE_OFF + r8(base_real)
+            ld = BASE_OFF + cpad(base_real)
             D = NHWC(P, h, w, ld, dtype, device)
             ent = self.dec[level]
             if prev is None:
                 second = feat.d(0, second_map)
             else:
                 pD, pflow, pbase = prev
-                fu = NHWC(P, h, w, 2, torch.float32, device)     # upflow
+                fu = NHWC(P, h, w, 8, torch.float32, device)     # upflow (2 ch; ld 8 for the 8-wide ConvT reads)
                 fe = NHWC(P, h, w, 2, torch.float32, device)     # upfeat
                 wt, bs = ent['upflow']
                 plan.add(f'pwc.dec{level}.upflow', lib.dbsr_conv_transpose_k4s2, P, pD.h, pD.w, 2, 2, pflow.d(0),
@@ -218,7 +231,7 @@ class PWCPlanner:
                 wt, bs = ent['upfeat']
                 plan.add(f'pwc.dec{level}.upfeat', lib.dbsr_conv_transpose_k4s2, P, pD.h, pD.w, BASE_OFF + pbase, 2,
                          pD.d(0), wt.data_ptr(), bs.data_ptr(), fe.d(0))
-                ws = NHWC(P, h, w, r8(C), dtype, device)
+                ws = NHWC(P, h, w, cpad(C), dtype, device)
                 plan.add(f'pwc.dec{level}.backwarp', lib.dbsr_backwarp, P, h, w, C, feat.d(0, second_map), fu.d(0),
                          BACKWARP_SCALE[level], ws.d(0))
                 plan.add(f'pwc.dec{level}.assemble', lib.dbsr_pwc_assemble, P, h, w, C, feat.d(0, first_map), fu.d(0),
@@ -232,7 +245,7 @@ class PWCPlanner:
                 start = BASE_OFF if i == 0 else DENSE_OFF[i - 1]
                 plan.conv(f'pwc.dec{level}.dense{i}', pc, P, D, start, (h, w), D, off, L.ACT_LRELU, cin=cin)
                 cin += DENSE_OUT[i]
-            fl = NHWC(P, h, w, 2, torch.float32, device)
+            fl = NHWC(P, h, w, 8, torch.float32, device)    # 2 ch (ld 8: read by the next level's ConvT)
             plan.conv(f'pwc.dec{level}.flow', ent['flow'], P, D, 0, (h, w), None, 0, L.ACT_NONE, cin=cin,
                       y_desc=fl.d(0))
             plan.keep.extend([D, fl])
@@ -241,7 +254,7 @@ class PWCPlanner:
         D2, fl2, base2 = prev
         h, w = D2.h, D2.w
         chans = [128, 128, 128, 96, 64, 32]
-        bufs = [NHWC(P, h, w, r8(c), dtype, device) for c in chans]
+        bufs = [NHWC(P, h, w, cpad(c), dtype, device) for c in chans]
         x, xc0, cin = D2, 0, BASE_OFF + base2
         for i in range(6):
             plan.conv(f'pwc.refiner{i}', self.ref[i], P, x, xc0, (h, w), bufs[i], 0, L.ACT_LRELU, cin=cin)

@@ -20,7 +20,7 @@ def _nhwc(x, dtype=None):
     if dtype is not None:
         t = t.to(dtype)
     c = t.shape[-1]
-    ld = (c + 7) // 8 * 8
+    ld = (c + 7) // 8 * 8 if c <= 16 else (c + 31) // 32 * 32     # dbsr_conv2d channel padding
     out = torch.zeros(*t.shape[:-1], ld, dtype=t.dtype, device=t.device)
     out[..., :c] = t
     return out, ld
@@ -111,8 +111,8 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, act=L.ACT_NONE
     d.out_h, d.out_w = oh, ow
     d.act = act
     if residual is not None:
-        rr, _ = _nhwc(residual, ody)
-        d.res = L.tensor_desc(rr, ldy)
+        rr, ldr = _nhwc(residual, ody)
+        d.res = L.tensor_desc(rr, ldr)
     else:
         d.res = L.NULL_TENSOR
     d.post_act = post_act

@@ -79,14 +79,19 @@ typedef struct dbsr_conv_desc {
     int out_mode, shuffle;
 } dbsr_conv_desc;
 
-/* Packed weight layout: [cout_pad][kgp*8] with k-group kg = (ky*kw+kx)*(cin8/8) + c/8, where
- * cin8 = round_up(cin, 8), kgp = round_up(kh*kw*cin8/8, 4), cout_pad = round_up(cout, 64). */
+/* Packed weight layout: [cout_pad][kgp*8] with k-group kg = (ky*kw+kx)*(cinp/8) + c/8, where
+ * cinp = cin <= 16 ? round_up(cin, 8) : round_up(cin, 32), kgp = round_up(kh*kw*cinp/8, 4),
+ * cout_pad = round_up(cout, 64).  The conv reads input channels [c0, c0+cinp) of every pixel, so the
+ * caller's slice must extend that far and channels [cin, cinp) must hold finite values (zeros). */
 size_t dbsr_conv_packed_elems(int cout, int cin, int kh, int kw);
 /* w_f32: torch layout [cout][cin][kh][kw] fp32 (device).  bias_f32 may be NULL.  With shuffle > 1
  * the output channels are permuted for the DBSR_OUT_SHUFFLE epilogue (and bias_out likewise). */
 int dbsr_conv_pack_weights(const float* w_f32, const float* bias_f32, int cout, int cin, int kh, int kw,
                            int dtype, int shuffle, void* w_packed, float* bias_out, void* stream);
 int dbsr_conv2d(const dbsr_conv_desc* d, void* stream);
+/* Kernel selection for dbsr_conv2d: 1 (default) uses the LDS-tiled 3x3 kernel where it applies
+ * (3x3, stride 1, pad 1, dilation 1, cin % 32 == 0, NHWC out); 0 forces the generic kernel. */
+int dbsr_set_conv_algo(int tiled);
 
 /* 81-channel cost volume of (first, second) over displacements [-4,4]^2, divided by C, followed by
  * LeakyReLU(0.1) when leaky != 0.  first/second/out: NHWC slices; out channel (dy+4)*9+(dx+4). */
@@ -110,7 +115,8 @@ int dbsr_fuse_softmax(int B, int N, int hw, int c, dbsr_tensor logits, dbsr_tens
                       dbsr_tensor fused, dbsr_tensor weights, void* stream);
 
 /* ConvTranspose2d(cin -> cout<=4, k=4, s=2, p=1): in NHWC slice [n][h][w], out NHWC fp32 [n][2h][2w].
- * w: torch layout [cin][cout][4][4] fp32; bias [cout] fp32. */
+ * w: fp32 repacked as [ky][kx][cout][cin8] (torch's [cin][cout][4][4] permuted, channels zero-padded
+ * to cin8 = round_up(cin, 8)); bias [cout] fp32.  Reads input channels [c0, c0+cin8). */
 int dbsr_conv_transpose_k4s2(int n, int h, int w, int cin, int cout, dbsr_tensor in, const float* wgt,
                              const float* bias, dbsr_tensor out, void* stream);
 

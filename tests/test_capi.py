@@ -42,8 +42,10 @@ def test_struct_layout_matches_c():
 
 
 def test_packed_size(L):
-    # cin 117 -> 120 (15 groups of 8) * 9 taps = 135 -> 136 k-groups; cout 128 -> 128 rows
-    assert L.lib().dbsr_conv_packed_elems(128, 117, 3, 3) == 128 * 136 * 8
+    # cin 117 -> 128 (cin > 16 pads to 32: 16 groups of 8) * 9 taps = 144 k-groups; cout 128 -> 128 rows
+    assert L.lib().dbsr_conv_packed_elems(128, 117, 3, 3) == 128 * 144 * 8
+    # cin 4 -> 8 (1 group) * 9 taps = 9 -> 12 k-groups; cout 64
+    assert L.lib().dbsr_conv_packed_elems(64, 4, 3, 3) == 64 * 12 * 8
     assert L.lib().dbsr_conv_packed_elems(3, 32, 1, 1) == 64 * 4 * 8
 
 

@@ -74,6 +74,9 @@ CONV_CASES = [
     (2, 32, 16, 16, 2, 3, 1, 1, 1),
     (2, 2, 10, 10, 64, 3, 1, 1, 1),
     (1, 32, 40, 24, 3, 1, 1, 0, 1),
+    (2, 32, 40, 24, 32, 3, 1, 1, 1),       # tiled kernel, 32-cout variant, partial tiles
+    (2, 192, 20, 17, 128, 3, 1, 1, 1),     # tiled kernel, 6 chunks, 2 cout tiles
+    (3, 128, 48, 48, 512, 3, 1, 1, 1),     # tiled kernel at the weight-predictor shape
 ]
 
 
@@ -101,6 +104,26 @@ def test_conv2d_bf16(ops, case):
     out = ops.conv2d(x.to(DEV), w.to(DEV), None, stride=s, padding=p, dilation=d,
                      compute_dtype=torch.bfloat16, out_f32=True).cpu()
     np.testing.assert_allclose(out.numpy(), ref.numpy(), atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('case', [(2, 64, 48, 48, 64), (2, 32, 70, 36, 32), (1, 128, 17, 33, 96)])
+def test_conv2d_tiled_vs_generic(ops, dtype, case):
+    from dbsr_amd import _lib
+    N, Cin, H, W, Cout = case
+    gen = torch.Generator().manual_seed(H * W)
+    x = torch.randn(N, Cin, H, W, generator=gen).to(DEV)
+    w = (torch.randn(Cout, Cin, 3, 3, generator=gen) / (Cin * 9) ** 0.5).to(DEV)
+    b = (torch.randn(Cout, generator=gen) * 0.1).to(DEV)
+    res = torch.randn(N, Cout, H, W, generator=gen).to(DEV)
+    outs = []
+    for algo in (1, 0):
+        _lib.lib().dbsr_set_conv_algo(algo)
+        outs.append(ops.conv2d(x, w, b, padding=1, act=1, residual=res, post_act=1, compute_dtype=dtype,
+                               out_f32=True).cpu())
+    _lib.lib().dbsr_set_conv_algo(1)
+    # same fp32 products in the same k order per output -> identical up to accumulation order
+    np.testing.assert_allclose(outs[0].numpy(), outs[1].numpy(), atol=1e-5, rtol=1e-5)
 
 
 def test_conv2d_residual_relu(ops):

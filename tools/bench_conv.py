@@ -1,0 +1,45 @@
+"""Microbenchmark of dbsr_conv2d on the cfg2 hot shapes: tiled vs generic kernel, bf16.
+Usage: python tools/bench_conv.py"""
+import os
+import sys
+import torch
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from dbsr_amd import _lib as L                     # noqa: E402
+from dbsr_amd.engine import NHWC, PackedConv, Plan  # noqa: E402
+
+SHAPES = [  # name, frames, H, W, cin, cout, k
+    ('enc.res 64->64', 112, 48, 48, 64, 64, 3),
+    ('enc.out 64->512', 112, 48, 48, 64, 512, 3),
+    ('wp.init 192->128', 112, 48, 48, 192, 128, 3),
+    ('wp.res 128->128', 112, 48, 48, 128, 128, 3),
+    ('wp.out 128->512', 112, 48, 48, 128, 512, 3),
+    ('dec.post 32->32', 8, 384, 384, 32, 32, 3),
+    ('dec.pre 64->64', 8, 48, 48, 64, 64, 3),
+]
+
+
+def main():
+    dev = torch.device('cuda')
+    dt = torch.bfloat16
+    s = torch.cuda.current_stream().cuda_stream
+    for name, F, H, W, cin, cout, k in SHAPES:
+        conv = torch.nn.Conv2d(cin, cout, k, padding=k // 2).to(dev)
+        pc = PackedConv(conv, dt, dev, s)
+        x = NHWC(F, H, W, cin, dt, dev)
+        x.t.normal_()
+        y = NHWC(F, H, W, cout, dt, dev)
+        plan = Plan()
+        plan.conv(name, pc, F, x, 0, (H, W), y, 0, L.ACT_RELU)
+        flop = plan.work[0][1]
+        res = []
+        for algo in (1, 0):
+            L.lib().dbsr_set_conv_algo(algo)
+            ms = plan.time_ops(s, reps=20)[0][1]
+            res.append((ms, flop / ms / 1e9))
+        L.lib().dbsr_set_conv_algo(1)
+        print(f'{name:20s} tiled {res[0][0]*1e3:8.1f} us {res[0][1]:7.1f} TF/s | generic {res[1][0]*1e3:8.1f} us '
+              f'{res[1][1]:7.1f} TF/s | x{res[1][0]/res[0][0]:.2f}')
+
+
+if __name__ == '__main__':
+    main()
