@@ -18,6 +18,8 @@
 // ResBlock residual (+ReLU) and the PixelShuffle epilogue of the decoder upsampler.
 #include "common.hpp"
 
+#include <algorithm>
+
 using namespace dbsr;
 
 namespace {
@@ -27,7 +29,7 @@ inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
 // conv with cin > 16 is a whole number of 32-channel MFMA chunks per tap
 inline int cin_pad(int cin) { return cin <= 16 ? round_up(cin, 8) : round_up(cin, 32); }
 
-int g_tiled_enabled = 1;   // dbsr_set_conv_algo(0) forces the generic kernel (A/B testing)
+int g_tiled_enabled = 1;   // dbsr_set_conv_algo: 0 generic only, 1 LDS-tiled where applicable
 
 struct ConvK {
     const void* x; long long x_is; int x_ld; dbsr_frame_map xm; int in_h, in_w;
@@ -67,6 +69,20 @@ __device__ __forceinline__ f32x4_t mma(const Frag<float>& A, const Frag<float>& 
     c = __builtin_amdgcn_mfma_f32_16x16x4f32(A.b.z, B.b.z, c, 0, 0, 0);
     c = __builtin_amdgcn_mfma_f32_16x16x4f32(A.b.w, B.b.w, c, 0, 0, 0);
     return c;
+}
+
+// bias of output channels co..co+3, loaded unconditionally from clamped indices (a per-element
+// conditional load makes hipcc branch and wait vmcnt(0) per element); 0 past cout or without bias
+__device__ __forceinline__ f32x4_t load_bias4(const ConvK& k, int co) {
+    f32x4_t b = {0.f, 0.f, 0.f, 0.f};
+    if (k.bias) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float v = k.bias[min(co + r, k.cout - 1)];
+            b[r] = co + r < k.cout ? v : 0.f;
+        }
+    }
+    return b;
 }
 
 template <typename T>
@@ -123,6 +139,9 @@ __global__ __launch_bounds__(256) void conv2d_kernel(ConvK k) {
     const T* wr[MT];
 #pragma unroll
     for (int i = 0; i < MT; ++i) wr[i] = (const T*)k.w + (long long)(c_base + i * 16 + col) * k.Kp + kgl * 8;
+    f32x4_t bias[MT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) bias[i] = load_bias4(k, c_base + i * 16 + kgl * 4);
 
     f32x4_t acc[MT][NT];
 #pragma unroll
@@ -160,26 +179,12 @@ __global__ __launch_bounds__(256) void conv2d_kernel(ConvK k) {
 #pragma unroll
             for (int j = 0; j < NT; ++j) acc[i][j] = mma(a[i], b[j], acc[i][j]);
     };
-    if constexpr (sizeof(T) == 2) {
-        // one k-step of register prefetch: the loads of step s+1 are in flight during step s's MFMAs
-        Frag<T> a0[MT], b0[NT], a1[MT], b1[NT];
-        load(0, a0, b0);
-        int ks = 0;
-        for (; ks + 1 < nks; ks += 2) {
-            load(ks + 1, a1, b1);
-            compute(a0, b0);
-            if (ks + 2 < nks) load(ks + 2, a0, b0);
-            compute(a1, b1);
-        }
-        if (ks < nks) compute(a0, b0);
-    } else {
-        // fp32 (parity mode): fragments are twice as wide; no prefetch (the prefetched variant also
-        // trips a ROCm 7.2 machine-copy-propagation crash)
-        for (int ks = 0; ks < nks; ++ks) {
-            Frag<T> a0[MT], b0[NT];
-            load(ks, a0, b0);
-            compute(a0, b0);
-        }
+    // (a one-k-step register prefetch was measured slower here: it cost occupancy on the large 1x1
+    // convs without helping the latency-bound tiny ones)
+    for (int ks = 0; ks < nks; ++ks) {
+        Frag<T> a0[MT], b0[NT];
+        load(ks, a0, b0);
+        compute(a0, b0);
     }
 
     // epilogue: bias, activation, residual, post-activation, store
@@ -196,11 +201,7 @@ __global__ __launch_bounds__(256) void conv2d_kernel(ConvK k) {
             const int nvalid = min(4, k.cout - co);
             float v[4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                float t = acc[i][j][r];
-                if (k.bias && r < nvalid) t += k.bias[co + r];
-                v[r] = apply_act(t, k.act);
-            }
+            for (int r = 0; r < 4; ++r) v[r] = apply_act(acc[i][j][r] + bias[i][r], k.act);
             if (k.out_mode == DBSR_OUT_NHWC) {
                 if (k.r) {
                     const long long roff = map_frame(k.rm, f) * k.r_is + (long long)rr * k.r_ld + k.r_c0 + co;
@@ -278,11 +279,15 @@ __global__ void pack_weights_kernel(const float* __restrict__ w, const float* __
 template <typename T, int WM, int WN>
 struct TileCfg {
     static constexpr int TW = 16, TH = 4 * WN / 16, HWD = TW + 2, HHT = TH + 2;
-    static constexpr int NQ = HHT * HWD;
+    static constexpr int NQ = HHT * HWD;                      // halo pixels
+    static constexpr int NQP = (NQ + 63) / 64 * 64;           // plane length (pixels): whole 1-KiB pieces
     static constexpr int HALVES = sizeof(T) / 2;              // 16-B halves per k-group (bf16 1, f32 2)
-    static constexpr int IN_ITEMS = (NQ + 15) / 16 * HALVES;  // 1-KiB LDS pieces: (16-pixel block, half)
-    static constexpr int W_ITEMS = 9 * (WM / 16) * HALVES;    // 1-KiB LDS pieces: (tap, 16-cout block, half)
-    static constexpr int IN_U4 = IN_ITEMS * 64, W_U4 = W_ITEMS * 64;
+    static constexpr int PLANES = 4 * HALVES;                 // (k-group, half)
+    static constexpr int IN_ITEMS = PLANES * (NQP / 64);      // 1-KiB LDS-DMA pieces of the halo tile
+    static constexpr int W_ITEMS = 9 * (WM / 16) * HALVES;    // 1-KiB pieces: (tap, 16-cout block, half)
+    static constexpr int IN_U4 = PLANES * NQP, W_U4 = W_ITEMS * 64;
+    static constexpr int NPIX = 4 * WN;                       // output pixels per tile
+    static constexpr int OSTR = WM * (int)sizeof(T) + 16;     // staged-output pixel stride (bytes)
 };
 
 // 16 zero bytes per lane for halo pixels outside the frame (LDS-DMA cannot write zeros itself)
@@ -296,10 +301,11 @@ template <typename T, int WM, int WN>
 __global__ __launch_bounds__(256, 2) void conv3x3_tiled_kernel(ConvK k, int tiles_x, int tiles_y, int nct,
                                                                int nblocks) {
     using C = TileCfg<T, WM, WN>;
+    static_assert(C::NPIX * C::OSTR <= (C::IN_U4 + C::W_U4) * 16, "output staging must fit the LDS tile");
     // One LDS array (a second __shared__ object can de-pipeline LDS-DMA: cdna_hip_programming.md §5 item 4a)
     __shared__ __attribute__((aligned(16))) u32x4_t lds[C::IN_U4 + C::W_U4];
-    u32x4_t* lin = lds;                 // [pixel block][half][g][16 px] x 16 B
-    u32x4_t* lw = lds + C::IN_U4;       // [tap][cout block][half][g][16 co] x 16 B
+    u32x4_t* lin = lds;                 // [k-group][half][NQP halo pixels] x 16 B  (planar)
+    u32x4_t* lw = lds + C::IN_U4;       // [tap][cout block][half][k-group][16 co] x 16 B
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int g = lane >> 4, col = lane & 15;
@@ -318,19 +324,26 @@ __global__ __launch_bounds__(256, 2) void conv3x3_tiled_kernel(ConvK k, int tile
 
     const T* xf = (const T*)k.x + map_frame(k.xm, f) * k.x_is;
     const int nchunks = k.CG / 4;
+    f32x4_t bias[WM / 16];
+#pragma unroll
+    for (int i = 0; i < WM / 16; ++i) bias[i] = load_bias4(k, c_base + i * 16 + g * 4);
 
-    // Stage one 32-channel chunk: every wave-instruction moves one 1-KiB piece, lane l -> (k-group l>>4,
-    // pixel/cout l&15), so the LDS image is lane-linear (LDS-DMA) and 16 consecutive rows of a plane
-    // occupy 16 distinct 16-B bank slots (conflict-free ds_read_b128 for any tap shift).
+    // Stage one 32-channel chunk by LDS-DMA (16 B per lane, lane-linear destination):
+    //  halo: one piece = 64 consecutive pixels of one (k-group, half) plane; pixels outside the frame
+    //        read the zero page.  Planes are 1-KiB multiples, so the 16 pixels a ds_read_b128 lane group
+    //        reads are 16 distinct bank slots for every tap shift (conflict-free), and a pixel's
+    //        address is linear in the tap shift (immediate-offset reads).
+    //  weights: one piece = 16 output channels x 4 k-groups of one tap (16 x 64 contiguous bytes).
     auto issue = [&](int chunk) {
         for (int item = wave; item < C::IN_ITEMS; item += 4) {
-            const int qb = item / C::HALVES, h = item % C::HALVES;
-            const int q = qb * 16 + col;
+            const int plane = item / (C::NQP / 64), seg = item % (C::NQP / 64);
+            const int gg = plane / C::HALVES, h = plane % C::HALVES;
+            const int q = seg * 64 + lane;
             const void* src = g_dbsr_zero16;
             if (q < C::NQ) {
                 const int iy = y0 - 1 + q / C::HWD, ix = x0 - 1 + q % C::HWD;
                 if ((unsigned)iy < (unsigned)k.in_h && (unsigned)ix < (unsigned)k.in_w)
-                    src = xf + ((long long)iy * k.in_w + ix) * k.x_ld + chunk * 32 + g * 8 + h * 4;
+                    src = xf + ((long long)iy * k.in_w + ix) * k.x_ld + chunk * 32 + gg * 8 + h * 4;
             }
             glds16(src, lin + item * 64);
         }
@@ -349,43 +362,135 @@ __global__ __launch_bounds__(256, 2) void conv3x3_tiled_kernel(ConvK k, int tile
         for (int j = 0; j < WN / 16; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
     const int row0 = wave * (WN / 16);
+    // lane-dependent LDS bases; every tap/fragment offset below is a compile-time immediate
+    const u32x4_t* lb_in = lin + (g * C::HALVES) * C::NQP + row0 * C::HWD + col;
+    const u32x4_t* lb_w = lw + g * 16 + col;
+    auto read_frags = [&](int tap, Frag<T> (&a)[WM / 16], Frag<T> (&b)[WN / 16]) {
+        const int ky = tap / 3, kx = tap % 3;
+#pragma unroll
+        for (int i = 0; i < WM / 16; ++i) {
+            const u32x4_t* p = lb_w + ((tap * (WM / 16) + i) * C::HALVES) * 64;
+            if constexpr (sizeof(T) == 2) {
+                a[i].v = __builtin_bit_cast(bf16x8_t, p[0]);
+            } else {
+                a[i].a = __builtin_bit_cast(float4, p[0]);
+                a[i].b = __builtin_bit_cast(float4, p[64]);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < WN / 16; ++j) {
+            const u32x4_t* p = lb_in + (j + ky) * C::HWD + kx;
+            if constexpr (sizeof(T) == 2) {
+                b[j].v = __builtin_bit_cast(bf16x8_t, p[0]);
+            } else {
+                b[j].a = __builtin_bit_cast(float4, p[0]);
+                b[j].b = __builtin_bit_cast(float4, p[C::NQP]);
+            }
+        }
+    };
+    auto mfmas = [&](const Frag<T> (&a)[WM / 16], const Frag<T> (&b)[WN / 16]) {
+#pragma unroll
+        for (int i = 0; i < WM / 16; ++i)
+#pragma unroll
+            for (int j = 0; j < WN / 16; ++j) acc[i][j] = mma(a[i], b[j], acc[i][j]);
+    };
+
     for (int chunk = 0; chunk < nchunks; ++chunk) {
         issue(chunk);
         __syncthreads();                 // vmcnt(0) for the LDS-DMA + barrier
-#pragma unroll 3
-        for (int tap = 0; tap < 9; ++tap) {
-            const int ky = tap / 3, kx = tap % 3;
-            Frag<T> a[WM / 16], b[WN / 16];
+        // taps software-pipelined through two fragment sets: tap t+1's ds_reads are in flight during
+        // tap t's MFMAs
+        Frag<T> a0[WM / 16], b0[WN / 16], a1[WM / 16], b1[WN / 16];
+        read_frags(0, a0, b0);
 #pragma unroll
-            for (int i = 0; i < WM / 16; ++i) {
-                const u32x4_t* p = lw + ((tap * (WM / 16) + i) * C::HALVES) * 64 + g * 16 + col;
-                if constexpr (sizeof(T) == 2) {
-                    a[i].v = __builtin_bit_cast(bf16x8_t, p[0]);
-                } else {
-                    a[i].a = __builtin_bit_cast(float4, p[0]);
-                    a[i].b = __builtin_bit_cast(float4, p[64]);
-                }
+        for (int tap = 0; tap < 9; tap += 2) {
+            if (tap + 1 < 9) read_frags(tap + 1, a1, b1);
+            mfmas(a0, b0);
+            if (tap + 1 < 9) {
+                if (tap + 2 < 9) read_frags(tap + 2, a0, b0);
+                mfmas(a1, b1);
             }
-#pragma unroll
-            for (int j = 0; j < WN / 16; ++j) {
-                const int q = (row0 + j + ky) * C::HWD + kx + col;
-                const u32x4_t* p = lin + ((q >> 4) * C::HALVES) * 64 + g * 16 + (q & 15);
-                if constexpr (sizeof(T) == 2) {
-                    b[j].v = __builtin_bit_cast(bf16x8_t, p[0]);
-                } else {
-                    b[j].a = __builtin_bit_cast(float4, p[0]);
-                    b[j].b = __builtin_bit_cast(float4, p[64]);
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < WM / 16; ++i)
-#pragma unroll
-                for (int j = 0; j < WN / 16; ++j) acc[i][j] = mma(a[i], b[j], acc[i][j]);
         }
         __syncthreads();                 // all waves done reading before the next chunk lands
     }
 
-    // ---- epilogue ----
+    // ---- epilogue: bias + act into an LDS [pixel][cout] tile, then whole 16-B rows per lane ----
+    const bool staged = !k.y_f32 && k.y_ld % 8 == 0 && k.y_c0 % 8 == 0 && k.cout % 8 == 0 &&
+                        (!k.r || (k.r_ld % 8 == 0 && k.r_c0 % 8 == 0));
+    if (staged) {
+        char* ob = (char*)lds;
+#pragma unroll
+        for (int j = 0; j < WN / 16; ++j) {
+            const int pix = (row0 + j) * C::TW + col;
+#pragma unroll
+            for (int i = 0; i < WM / 16; ++i) {
+                const int co = i * 16 + g * 4;
+                float v[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = apply_act(acc[i][j][r] + bias[i][r], k.act);
+                if constexpr (sizeof(T) == 2) {
+                    uint2 q;
+                    q.x = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
+                    q.y = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
+                    *(uint2*)(ob + pix * C::OSTR + co * 2) = q;
+                } else {
+                    *(float4*)(ob + pix * C::OSTR + co * 4) = make_float4(v[0], v[1], v[2], v[3]);
+                }
+            }
+        }
+        __syncthreads();
+        constexpr int EPC = 16 / (int)sizeof(T);                 // elements per 16-B chunk
+        constexpr int CPP = WM / EPC;                            // chunks per pixel
+        constexpr int NCH = C::NPIX * CPP;
+        constexpr int PER = (NCH + 255) / 256;
+        const int cvalid = min(WM, k.cout - c_base);
+        const T* rbase = k.r ? (const T*)k.r + map_frame(k.rm, f) * k.r_is + k.r_c0 + c_base : nullptr;
+        T* ybase = (T*)k.y + map_frame(k.ym, f) * k.y_is + k.y_c0 + c_base;
+        u32x4_t rv[PER];
+        long long off[PER];
+        bool ok[PER];
+#pragma unroll
+        for (int e = 0; e < PER; ++e) {
+            const int c = threadIdx.x + e * 256;
+            const int pix = c / CPP, sc = c % CPP;
+            const int oy = y0 + pix / C::TW, ox = x0 + pix % C::TW;
+            ok[e] = c < NCH && oy < k.out_h && ox < k.out_w && sc * EPC < cvalid;
+            off[e] = ok[e] ? ((long long)oy * k.out_w + ox) : 0;
+        }
+        if (rbase) {        // uniform; every residual load issued back to back (clamped address, no branches)
+#pragma unroll
+            for (int e = 0; e < PER; ++e) {
+                const int sc = (threadIdx.x + e * 256) % CPP;
+                rv[e] = *(const u32x4_t*)(rbase + off[e] * k.r_ld + (ok[e] ? sc * EPC : 0));
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < PER; ++e) {
+            if (!ok[e]) continue;
+            const int c = threadIdx.x + e * 256;
+            const int pix = c / CPP, sc = c % CPP;
+            u32x4_t val = *(const u32x4_t*)(ob + pix * C::OSTR + sc * 16);
+            if (rbase) {
+                if constexpr (sizeof(T) == 2) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const float lo = __uint_as_float(val[q] << 16) + __uint_as_float(rv[e][q] << 16);
+                        const float hi = __uint_as_float(val[q] & 0xffff0000u) + __uint_as_float(rv[e][q] & 0xffff0000u);
+                        val[q] = (unsigned)f2bf(apply_act(lo, k.post_act)) |
+                                 ((unsigned)f2bf(apply_act(hi, k.post_act)) << 16);
+                    }
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        val[q] = __float_as_uint(apply_act(__uint_as_float(val[q]) + __uint_as_float(rv[e][q]),
+                                                           k.post_act));
+                }
+            }
+            *(u32x4_t*)(ybase + off[e] * k.y_ld + sc * EPC) = val;
+        }
+        return;
+    }
+    // generic epilogue (fp32 output of a bf16 conv, unaligned slices): per-lane fragments
 #pragma unroll
     for (int j = 0; j < WN / 16; ++j) {
         const int oy = y0 + row0 + j, ox = x0 + col;
@@ -398,32 +503,12 @@ __global__ __launch_bounds__(256, 2) void conv3x3_tiled_kernel(ConvK k, int tile
             const int nvalid = min(4, k.cout - co);
             float v[4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                float t = acc[i][j][r];
-                if (k.bias && r < nvalid) t += k.bias[co + r];
-                v[r] = apply_act(t, k.act);
-            }
+            for (int r = 0; r < 4; ++r) v[r] = apply_act(acc[i][j][r] + bias[i][r], k.act);
             if (k.r) {
                 const long long roff = map_frame(k.rm, f) * k.r_is + (long long)rr * k.r_ld + k.r_c0 + co;
-                float rv[4] = {0.f, 0.f, 0.f, 0.f};
-                if (nvalid == 4 && k.vec_store) {
-                    if (k.y_f32) {
-                        float4 q = *(const float4*)((const float*)k.r + roff);
-                        rv[0] = q.x; rv[1] = q.y; rv[2] = q.z; rv[3] = q.w;
-                    } else if constexpr (sizeof(T) == 2) {
-                        uint2 q = *(const uint2*)((const T*)k.r + roff);
-                        rv[0] = __uint_as_float(q.x << 16); rv[1] = __uint_as_float(q.x & 0xffff0000u);
-                        rv[2] = __uint_as_float(q.y << 16); rv[3] = __uint_as_float(q.y & 0xffff0000u);
-                    } else {
-                        float4 q = *(const float4*)((const T*)k.r + roff);
-                        rv[0] = q.x; rv[1] = q.y; rv[2] = q.z; rv[3] = q.w;
-                    }
-                } else {
-                    for (int r = 0; r < nvalid; ++r)
-                        rv[r] = k.y_f32 ? ((const float*)k.r)[roff + r] : elem<T>::ld((const T*)k.r + roff + r);
-                }
-#pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] = apply_act(v[r] + rv[r], k.post_act);
+                for (int r = 0; r < nvalid; ++r)
+                    v[r] = apply_act(v[r] + (k.y_f32 ? ((const float*)k.r)[roff + r] : elem<T>::ld((const T*)k.r + roff + r)),
+                                     k.post_act);
             }
             store4<T>(k, map_frame(k.ym, f) * k.y_is + (long long)rr * k.y_ld + k.y_c0 + co, v, nvalid);
         }
@@ -487,8 +572,9 @@ int dispatch_conv(const ConvK& k, const dbsr_conv_desc* d, hipStream_t s) {
 
 }  // namespace
 
-extern "C" int dbsr_set_conv_algo(int tiled) {
-    g_tiled_enabled = tiled ? 1 : 0;
+extern "C" int dbsr_set_conv_algo(int algo) {
+    DBSR_CHECK_ARG(algo >= 0 && algo <= 1, "set_conv_algo: 0 generic, 1 tiled");
+    g_tiled_enabled = algo;
     return 0;
 }
 

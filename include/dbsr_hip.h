@@ -89,9 +89,10 @@ size_t dbsr_conv_packed_elems(int cout, int cin, int kh, int kw);
 int dbsr_conv_pack_weights(const float* w_f32, const float* bias_f32, int cout, int cin, int kh, int kw,
                            int dtype, int shuffle, void* w_packed, float* bias_out, void* stream);
 int dbsr_conv2d(const dbsr_conv_desc* d, void* stream);
-/* Kernel selection for dbsr_conv2d: 1 (default) uses the LDS-tiled 3x3 kernel where it applies
- * (3x3, stride 1, pad 1, dilation 1, cin % 32 == 0, NHWC out); 0 forces the generic kernel. */
-int dbsr_set_conv_algo(int tiled);
+/* Kernel selection for dbsr_conv2d (process-wide; for A/B testing): 1 (default) = LDS-tiled 3x3
+ * kernel where it applies (3x3, stride 1, pad 1, dilation 1, cin > 16, out >= 8x8, NHWC out),
+ * 0 = generic implicit-GEMM kernel only. */
+int dbsr_set_conv_algo(int algo);
 
 /* 81-channel cost volume of (first, second) over displacements [-4,4]^2, divided by C, followed by
  * LeakyReLU(0.1) when leaky != 0.  first/second/out: NHWC slices; out channel (dy+4)*9+(dx+4). */

@@ -119,11 +119,11 @@ def test_conv2d_tiled_vs_generic(ops, dtype, case):
     outs = []
     for algo in (1, 0):
         _lib.lib().dbsr_set_conv_algo(algo)
-        outs.append(ops.conv2d(x, w, b, padding=1, act=1, residual=res, post_act=1, compute_dtype=dtype,
-                               out_f32=True).cpu())
+        outs.append(ops.conv2d(x, w, b, padding=1, act=1, residual=res, post_act=1, compute_dtype=dtype).float().cpu())
     _lib.lib().dbsr_set_conv_algo(1)
-    # same fp32 products in the same k order per output -> identical up to accumulation order
-    np.testing.assert_allclose(outs[0].numpy(), outs[1].numpy(), atol=1e-5, rtol=1e-5)
+    # same products, fp32 accumulation, different summation order; outputs rounded to dtype
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    np.testing.assert_allclose(outs[0].numpy(), outs[1].numpy(), atol=tol, rtol=tol)
 
 
 def test_conv2d_residual_relu(ops):
