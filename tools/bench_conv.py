@@ -5,7 +5,7 @@ import sys
 import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from dbsr_amd import _lib as L                     # noqa: E402
-from dbsr_amd.engine import NHWC, PackedConv, Plan  # noqa: E402
+from dbsr_amd.engine import NHWC, PackedConv, Plan, cpad  # noqa: E402
 
 SHAPES = [  # name, frames, H, W, cin, cout, k
     ('enc.res 64->64', 112, 48, 48, 64, 64, 3),
@@ -31,12 +31,12 @@ def main():
     for name, F, H, W, cin, cout, k in SHAPES:
         conv = torch.nn.Conv2d(cin, cout, k, padding=k // 2).to(dev)
         pc = PackedConv(conv, dt, dev, s)
-        x = NHWC(F, H, W, cin, dt, dev)
+        x = NHWC(F, H, W, cpad(cin), dt, dev)
         x.t.normal_()
-        y = NHWC(F, H, W, cout, dt, dev)
+        y = NHWC(F, H, W, max(8, (cout + 7) // 8 * 8), dt, dev)
         plan = Plan()
         if 'res' in name or 'post' in name or 'pre' in name:
-            r = NHWC(F, H, W, cout, dt, dev)
+            r = NHWC(F, H, W, max(8, (cout + 7) // 8 * 8), dt, dev)
             plan.conv(name, pc, F, x, 0, (H, W), y, 0, L.ACT_NONE, res=r, post_act=L.ACT_RELU)
         else:
             plan.conv(name, pc, F, x, 0, (H, W), y, 0, L.ACT_RELU)

@@ -1,0 +1,19 @@
+#!/bin/bash
+# Profiling recipe run on the GPU box (see DESIGN.md "Measurement"):
+#   1. kernel trace + stats of the default bench workload
+#   2. separate PMC passes (FETCH_SIZE, WRITE_SIZE) restricted to the HBM-bound kernels
+# Usage: bash tools/profile.sh <tag>      (outputs under gpurun_out/prof_<tag>/)
+set -o pipefail
+tag=${1:-r01}
+out=gpurun_out/prof_$tag
+mkdir -p $out
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace -o run --output-format csv -- \
+    python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > $out/bench_trace.log 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "warp_kernel|fuse_softmax|conv3x3_tiled" \
+    -d $out/pmc_fetch -o run --output-format csv -- \
+    python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > $out/bench_fetch.log 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "warp_kernel|fuse_softmax|conv3x3_tiled" \
+    -d $out/pmc_write -o run --output-format csv -- \
+    python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > $out/bench_write.log 2>&1 || exit $?
+echo done

@@ -1,0 +1,61 @@
+"""Summarise a tools/profile.sh run into profiles/<tag>_summary.md (+ the raw kernel stats CSV).
+
+HBM traffic per launch = 2 x FETCH_SIZE + WRITE_SIZE (KB units, x1024), following
+MI355X_MICROARCH.md §HBM: on gfx950 FETCH_SIZE counts half of the bytes of 16-B-per-lane streaming
+reads, so it is doubled; WRITE_SIZE is exact for 16-B streaming stores.  Each counter comes from its
+own rocprofv3 --pmc pass (no trace domains combined).
+
+Usage: python tools/summarize_profile.py gpurun_out/prof_r01 r01
+"""
+import csv
+import os
+import shutil
+import statistics
+import sys
+
+KERNELS = {   # label -> (name predicate, algorithmic bytes per launch at the default bench workload)
+    'warp_kernel (DBSR warp, encoders.py:80)': (lambda n: n.startswith('void (anonymous namespace)::warp_kernel'), None),
+    'fuse_softmax_kernel (merging.py:116-126)': (lambda n: 'fuse_softmax_kernel' in n, None),
+}
+
+
+def main():
+    src, tag = sys.argv[1], sys.argv[2]
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    outdir = os.path.join(repo, 'profiles')
+    os.makedirs(outdir, exist_ok=True)
+    stats = list(csv.DictReader(open(os.path.join(src, 'trace', 'run_kernel_stats.csv'))))
+    shutil.copy(os.path.join(src, 'trace', 'run_kernel_stats.csv'), os.path.join(outdir, f'{tag}_kernel_stats.csv'))
+    lines = [f'# rocprofv3 summary {tag}', '',
+             'Command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline`',
+             '(bf16, batch 8 x 14 frames x 48x48; includes bench.py\'s per-op timing pass, so call counts are not',
+             'one forward). Full CSV: `%s_kernel_stats.csv`.' % tag, '',
+             '| kernel | calls | total ms | avg us | % |', '|---|---|---|---|---|']
+    for r in stats[:25]:
+        lines.append('| `%s` | %s | %.2f | %.1f | %s |' % (r['Name'][:110], r['Calls'], float(r['TotalDurationNs']) / 1e6,
+                                                        float(r['AverageNs']) / 1e3, r['Percentage']))
+    fetch = list(csv.DictReader(open(os.path.join(src, 'pmc_fetch', 'run_counter_collection.csv'))))
+    write = list(csv.DictReader(open(os.path.join(src, 'pmc_write', 'run_counter_collection.csv'))))
+    lines += ['', '## HBM traffic (PMC, separate passes)', '',
+              '| kernel | dispatches | FETCH_SIZE x2 (MB) | WRITE_SIZE (MB) | traffic/launch (MB) | avg dur (us) |',
+              '|---|---|---|---|---|---|']
+    for label, (pred, _) in KERNELS.items():
+        fr = [r for r in fetch if pred(r['Kernel_Name'])]
+        wr = [r for r in write if pred(r['Kernel_Name'])]
+        if not fr or not wr:
+            continue
+        # the large (bench-shaped) launches only
+        big = max(int(r['Grid_Size']) for r in fr)
+        fv = [float(r['Counter_Value']) for r in fr if int(r['Grid_Size']) == big]
+        wv = [float(r['Counter_Value']) for r in wr if int(r['Grid_Size']) == big]
+        dur = [int(r['End_Timestamp']) - int(r['Start_Timestamp']) for r in fr if int(r['Grid_Size']) == big]
+        fmb = 2 * statistics.median(fv) * 1024 / 1e6
+        wmb = statistics.median(wv) * 1024 / 1e6
+        lines.append('| %s | %d | %.1f | %.1f | %.1f | %.1f |' % (label, len(fv), fmb, wmb, fmb + wmb,
+                                                                statistics.median(dur) / 1e3))
+    open(os.path.join(outdir, f'{tag}_summary.md'), 'w').write('\n'.join(lines) + '\n')
+    print('\n'.join(lines))
+
+
+if __name__ == '__main__':
+    main()
