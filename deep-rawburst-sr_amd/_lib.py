@@ -66,6 +66,7 @@ def lib():
                                         c_void_p, c_void_p], c_int),
             'dbsr_conv2d': ([ctypes.POINTER(ConvDesc), c_void_p], c_int),
             'dbsr_set_conv_algo': ([c_int], c_int),
+            'dbsr_conv_kernel_for': ([ctypes.POINTER(ConvDesc)], c_int),
             'dbsr_correlation': ([c_int, c_int, c_int, c_int, Tensor, Tensor, Tensor, c_int, c_void_p], c_int),
             'dbsr_backwarp': ([c_int, c_int, c_int, c_int, Tensor, Tensor, c_float, Tensor, c_void_p], c_int),
             'dbsr_warp_bilinear': ([c_int, c_int, c_int, c_int, Tensor, c_void_p, c_ll, Tensor, c_void_p], c_int),
@@ -92,7 +93,7 @@ def lib():
 
 
 EXPORTED = ['dbsr_abi_version', 'dbsr_last_error', 'dbsr_conv_packed_elems', 'dbsr_conv_pack_weights', 'dbsr_conv2d',
-            'dbsr_set_conv_algo',
+            'dbsr_set_conv_algo', 'dbsr_conv_kernel_for',
             'dbsr_correlation', 'dbsr_backwarp', 'dbsr_warp_bilinear', 'dbsr_fuse_softmax',
             'dbsr_conv_transpose_k4s2', 'dbsr_pack_burst', 'dbsr_flow_finalize', 'dbsr_gauss_blur3',
             'dbsr_merge_prep', 'dbsr_pwc_assemble', 'dbsr_zero']

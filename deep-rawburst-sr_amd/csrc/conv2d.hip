@@ -539,12 +539,14 @@ int launch_conv(const ConvK& k, hipStream_t s) {
     return 0;
 }
 
+bool use_tiled(const dbsr_conv_desc* d) {
+    return d->kh == 3 && d->kw == 3 && d->stride == 1 && d->pad == 1 && d->dil == 1 && d->cin > 16 &&
+           d->out_h >= 8 && d->out_w >= 8 && d->out_mode == DBSR_OUT_NHWC && g_tiled_enabled;
+}
+
 template <typename T>
 int dispatch_conv(const ConvK& k, const dbsr_conv_desc* d, hipStream_t s) {
-    const bool tiled_ok = d->kh == 3 && d->kw == 3 && d->stride == 1 && d->pad == 1 && d->dil == 1 &&
-                          d->cin > 16 && d->out_h >= 8 && d->out_w >= 8 && d->out_mode == DBSR_OUT_NHWC &&
-                          g_tiled_enabled;
-    if (tiled_ok) {
+    if (use_tiled(d)) {
         if (k.cout <= 32) return launch_tiled<T, 32, 128>(k, d->n_frames, s);
         return launch_tiled<T, 64, 64>(k, d->n_frames, s);
     }
@@ -571,6 +573,11 @@ int dispatch_conv(const ConvK& k, const dbsr_conv_desc* d, hipStream_t s) {
 }
 
 }  // namespace
+
+extern "C" int dbsr_conv_kernel_for(const dbsr_conv_desc* d) {
+    if (!d) return -1;
+    return use_tiled(d) ? 1 : 0;
+}
 
 extern "C" int dbsr_set_conv_algo(int algo) {
     DBSR_CHECK_ARG(algo >= 0 && algo <= 1, "set_conv_algo: 0 generic, 1 tiled");

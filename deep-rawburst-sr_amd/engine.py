@@ -103,6 +103,7 @@ class Plan:
         self.ops = []        # (callable, args, name)
         self.keep = []
         self.work = {}       # op index -> ('flop' | 'byte', algorithmic amount per launch)
+        self.kernel = {}     # op index -> kernel family (convs)
 
     def add(self, name, fn, *args, work=None):
         if work is not None:
@@ -130,6 +131,7 @@ class Plan:
         self.keep.append(d)
         flop = 2.0 * n_frames * oh * ow * pc.cout * d.cin * pc.kh * pc.kw
         self.add(name, L.lib().dbsr_conv2d, ctypes.byref(d), work=('flop', flop))
+        self.kernel[len(self.ops) - 1] = 'conv3x3_tiled' if L.lib().dbsr_conv_kernel_for(d) == 1 else 'conv2d_generic'
         return d
 
     def run(self, stream):

@@ -93,6 +93,8 @@ int dbsr_conv2d(const dbsr_conv_desc* d, void* stream);
  * kernel where it applies (3x3, stride 1, pad 1, dilation 1, cin > 16, out >= 8x8, NHWC out),
  * 0 = generic implicit-GEMM kernel only. */
 int dbsr_set_conv_algo(int algo);
+/* Which kernel dbsr_conv2d would launch for `d` under the current selection: 1 LDS-tiled, 0 generic. */
+int dbsr_conv_kernel_for(const dbsr_conv_desc* d);
 
 /* 81-channel cost volume of (first, second) over displacements [-4,4]^2, divided by C, followed by
  * LeakyReLU(0.1) when leaky != 0.  first/second/out: NHWC slices; out channel (dy+4)*9+(dx+4). */
