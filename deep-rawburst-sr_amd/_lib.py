@@ -39,7 +39,8 @@ class ConvDesc(ctypes.Structure):
                 ('y', Tensor), ('out_h', ctypes.c_int), ('out_w', ctypes.c_int),
                 ('act', ctypes.c_int),
                 ('res', Tensor), ('post_act', ctypes.c_int),
-                ('out_mode', ctypes.c_int), ('shuffle', ctypes.c_int)]
+                ('out_mode', ctypes.c_int), ('shuffle', ctypes.c_int),
+                ('workspace', ctypes.c_void_p), ('workspace_bytes', ctypes.c_size_t), ('precise', ctypes.c_int)]
 
 
 _lib = None
@@ -67,6 +68,7 @@ def lib():
             'dbsr_conv2d': ([ctypes.POINTER(ConvDesc), c_void_p], c_int),
             'dbsr_set_conv_algo': ([c_int], c_int),
             'dbsr_conv_kernel_for': ([ctypes.POINTER(ConvDesc)], c_int),
+            'dbsr_conv_workspace_bytes': ([ctypes.POINTER(ConvDesc)], c_size_t),
             'dbsr_correlation': ([c_int, c_int, c_int, c_int, Tensor, Tensor, Tensor, c_int, c_void_p], c_int),
             'dbsr_backwarp': ([c_int, c_int, c_int, c_int, Tensor, Tensor, c_float, Tensor, c_void_p], c_int),
             'dbsr_warp_bilinear': ([c_int, c_int, c_int, c_int, Tensor, c_void_p, c_ll, Tensor, c_void_p], c_int),
@@ -93,7 +95,7 @@ def lib():
 
 
 EXPORTED = ['dbsr_abi_version', 'dbsr_last_error', 'dbsr_conv_packed_elems', 'dbsr_conv_pack_weights', 'dbsr_conv2d',
-            'dbsr_set_conv_algo', 'dbsr_conv_kernel_for',
+            'dbsr_set_conv_algo', 'dbsr_conv_kernel_for', 'dbsr_conv_workspace_bytes',
             'dbsr_correlation', 'dbsr_backwarp', 'dbsr_warp_bilinear', 'dbsr_fuse_softmax',
             'dbsr_conv_transpose_k4s2', 'dbsr_pack_burst', 'dbsr_flow_finalize', 'dbsr_gauss_blur3',
             'dbsr_merge_prep', 'dbsr_pwc_assemble', 'dbsr_zero']

@@ -40,6 +40,9 @@ struct ConvK {
     int out_mode, shuffle, cps;
     int npix;
     int vec_store;
+    int ksplit;        // K slices (generic kernel); > 1: fp32 partials to ws, summed by conv_splitk_finalize
+    float* ws;         // [ksplit][npix][cw] fp32
+    int cw;            // round_up(cout, 4)
 };
 
 template <typename T> struct Frag;
@@ -51,6 +54,13 @@ template <> struct Frag<bf16_t> {
 template <> struct Frag<float> {
     float4 a, b;
     __device__ __forceinline__ void load(const float* p) { a = *(const float4*)p; b = *(const float4*)(p + 4); }
+    __device__ __forceinline__ void load(const bf16_t* p) {      // bf16 activations, fp32 ("precise") math
+        const u32x4_t q = *(const u32x4_t*)p;
+        a = make_float4(__uint_as_float(q[0] << 16), __uint_as_float(q[0] & 0xffff0000u),
+                        __uint_as_float(q[1] << 16), __uint_as_float(q[1] & 0xffff0000u));
+        b = make_float4(__uint_as_float(q[2] << 16), __uint_as_float(q[2] & 0xffff0000u),
+                        __uint_as_float(q[3] << 16), __uint_as_float(q[3] & 0xffff0000u));
+    }
     __device__ __forceinline__ void zero() { a = make_float4(0, 0, 0, 0); b = a; }
 };
 
@@ -111,7 +121,40 @@ __device__ __forceinline__ void store4(const ConvK& k, long long off, const floa
     }
 }
 
-template <typename T, int MT, int NT>
+// bias + act (+ residual + post-act) of one pixel's 4 consecutive output channels, stored per out_mode
+template <typename T>
+__device__ __forceinline__ void epilogue_px(const ConvK& k, int p, int co, const f32x4_t& a, const f32x4_t& b) {
+    const int hw = k.out_h * k.out_w;
+    const int f = p / hw, rr = p - f * hw;
+    const int oy = rr / k.out_w, ox = rr - oy * k.out_w;
+    const int nvalid = min(4, k.cout - co);
+    float v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = apply_act(a[r] + b[r], k.act);
+    if (k.out_mode == DBSR_OUT_NHWC) {
+        if (k.r) {
+            const long long roff = map_frame(k.rm, f) * k.r_is + (long long)rr * k.r_ld + k.r_c0 + co;
+            if (k.y_f32) {
+                const float* rp = (const float*)k.r + roff;
+                for (int r = 0; r < nvalid; ++r) v[r] = apply_act(v[r] + rp[r], k.post_act);
+            } else {
+                const T* rp = (const T*)k.r + roff;
+                for (int r = 0; r < nvalid; ++r) v[r] = apply_act(v[r] + elem<T>::ld(rp + r), k.post_act);
+            }
+        }
+        store4<T>(k, map_frame(k.ym, f) * k.y_is + (long long)rr * k.y_ld + k.y_c0 + co, v, nvalid);
+    } else if (k.out_mode == DBSR_OUT_SHUFFLE) {
+        const int s = k.shuffle, sub = co / k.cps, c = co - sub * k.cps;
+        const int Y = oy * s + sub / s, X = ox * s + sub % s;
+        const long long off = map_frame(k.ym, f) * k.y_is + ((long long)Y * (k.out_w * s) + X) * k.y_ld + k.y_c0 + c;
+        store4<T>(k, off, v, nvalid);
+    } else {   // NCHW fp32
+        float* y = (float*)k.y + map_frame(k.ym, f) * k.y_is + (long long)co * hw + rr;
+        for (int r = 0; r < nvalid; ++r) y[(long long)r * hw] = v[r];
+    }
+}
+
+template <typename T, int MT, int NT, typename XT = T>
 __global__ __launch_bounds__(256) void conv2d_kernel(ConvK k) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int kgl = lane >> 4, col = lane & 15;
@@ -119,7 +162,7 @@ __global__ __launch_bounds__(256) void conv2d_kernel(ConvK k) {
     const int p_base = blockIdx.x * (4 * NT * 16) + wave * (NT * 16);
     const int c_base = blockIdx.y * (MT * 16);
 
-    const T* xb[NT];
+    const XT* xb[NT];
     int iy0[NT], ix0[NT];
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
@@ -127,11 +170,11 @@ __global__ __launch_bounds__(256) void conv2d_kernel(ConvK k) {
         if (p < k.npix) {
             const int f = p / hw, rr = p - f * hw;
             const int oy = rr / k.out_w, ox = rr - oy * k.out_w;
-            xb[j] = (const T*)k.x + map_frame(k.xm, f) * k.x_is;
+            xb[j] = (const XT*)k.x + map_frame(k.xm, f) * k.x_is;
             iy0[j] = oy * k.stride - k.pad;
             ix0[j] = ox * k.stride - k.pad;
         } else {
-            xb[j] = (const T*)k.x;
+            xb[j] = (const XT*)k.x;
             iy0[j] = -(1 << 28);
             ix0[j] = 0;
         }
@@ -149,11 +192,14 @@ __global__ __launch_bounds__(256) void conv2d_kernel(ConvK k) {
 #pragma unroll
         for (int j = 0; j < NT; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
+    // this block's K slice [ks0, ks1) (whole K without split)
+    const int nks_all = k.KGp >> 2;
+    const int ks0 = (int)((long long)nks_all * blockIdx.z / k.ksplit);
+    const int ks1 = (int)((long long)nks_all * (blockIdx.z + 1) / k.ksplit);
     // k-group decode of the next k-step to load, advanced incrementally by 4 per k-step
-    int tap = kgl / k.CG;
-    int cg = kgl - tap * k.CG;
+    int tap = (ks0 * 4 + kgl) / k.CG;
+    int cg = (ks0 * 4 + kgl) - tap * k.CG;
     int ky = tap / k.kw, kx = tap - (tap / k.kw) * k.kw;
-    const int nks = k.KGp >> 2;
     auto load = [&](int ks, Frag<T> (&a)[MT], Frag<T> (&b)[NT]) {
         const bool kval = ks * 4 + kgl < k.KG;
 #pragma unroll
@@ -181,51 +227,40 @@ __global__ __launch_bounds__(256) void conv2d_kernel(ConvK k) {
     };
     // (a one-k-step register prefetch was measured slower here: it cost occupancy on the large 1x1
     // convs without helping the latency-bound tiny ones)
-    for (int ks = 0; ks < nks; ++ks) {
+    for (int ks = ks0; ks < ks1; ++ks) {
         Frag<T> a0[MT], b0[NT];
         load(ks, a0, b0);
         compute(a0, b0);
     }
 
-    // epilogue: bias, activation, residual, post-activation, store
+    // epilogue: bias, activation, residual, post-activation, store (or fp32 partials under split-K)
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
         const int p = p_base + j * 16 + col;
         if (p >= k.npix) continue;
-        const int f = p / hw, rr = p - f * hw;
-        const int oy = rr / k.out_w, ox = rr - oy * k.out_w;
 #pragma unroll
         for (int i = 0; i < MT; ++i) {
             const int co = c_base + i * 16 + kgl * 4;
             if (co >= k.cout) continue;
-            const int nvalid = min(4, k.cout - co);
-            float v[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = apply_act(acc[i][j][r] + bias[i][r], k.act);
-            if (k.out_mode == DBSR_OUT_NHWC) {
-                if (k.r) {
-                    const long long roff = map_frame(k.rm, f) * k.r_is + (long long)rr * k.r_ld + k.r_c0 + co;
-                    if (k.y_f32) {
-                        const float* rp = (const float*)k.r + roff;
-                        for (int r = 0; r < nvalid; ++r) v[r] = apply_act(v[r] + rp[r], k.post_act);
-                    } else {
-                        const T* rp = (const T*)k.r + roff;
-                        for (int r = 0; r < nvalid; ++r) v[r] = apply_act(v[r] + elem<T>::ld(rp + r), k.post_act);
-                    }
-                }
-                store4<T>(k, map_frame(k.ym, f) * k.y_is + (long long)rr * k.y_ld + k.y_c0 + co, v, nvalid);
-            } else if (k.out_mode == DBSR_OUT_SHUFFLE) {
-                const int s = k.shuffle, sub = co / k.cps, c = co - sub * k.cps;
-                const int Y = oy * s + sub / s, X = ox * s + sub % s;
-                const long long off = map_frame(k.ym, f) * k.y_is +
-                                      ((long long)Y * (k.out_w * s) + X) * k.y_ld + k.y_c0 + c;
-                store4<T>(k, off, v, nvalid);
-            } else {   // NCHW fp32
-                float* y = (float*)k.y + map_frame(k.ym, f) * k.y_is + (long long)co * hw + rr;
-                for (int r = 0; r < nvalid; ++r) y[(long long)r * hw] = v[r];
-            }
+            if (k.ksplit > 1)
+                *(f32x4_t*)(k.ws + ((long long)blockIdx.z * k.npix + p) * k.cw + co) = acc[i][j];
+            else
+                epilogue_px<T>(k, p, co, acc[i][j], bias[i]);
         }
     }
+}
+
+// split-K finalize: sum the K-slice partials in slice order (deterministic), then the normal epilogue
+template <typename T>
+__global__ __launch_bounds__(256) void conv_splitk_finalize(ConvK k) {
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int groups = k.cw / 4;
+    if (idx >= (long long)k.npix * groups) return;
+    const int p = (int)(idx / groups), co = (int)(idx % groups) * 4;
+    if (co >= k.cout) return;
+    f32x4_t a = {0.f, 0.f, 0.f, 0.f};
+    for (int z = 0; z < k.ksplit; ++z) a += *(const f32x4_t*)(k.ws + ((long long)z * k.npix + p) * k.cw + co);
+    epilogue_px<T>(k, p, co, a, load_bias4(k, co));
 }
 
 __global__ void pack_weights_kernel(const float* __restrict__ w, const float* __restrict__ bias, int cout, int cin,
@@ -531,16 +566,53 @@ int launch_tiled(const ConvK& k, int n_frames, hipStream_t s) {
     return 0;
 }
 
-template <typename T, int MT, int NT>
+template <typename T, int MT, int NT, typename XT = T>
 int launch_conv(const ConvK& k, hipStream_t s) {
-    dim3 grid((k.npix + 4 * NT * 16 - 1) / (4 * NT * 16), (k.cout + MT * 16 - 1) / (MT * 16));
-    hipLaunchKernelGGL((conv2d_kernel<T, MT, NT>), grid, dim3(256), 0, s, k);
+    dim3 grid((k.npix + 4 * NT * 16 - 1) / (4 * NT * 16), (k.cout + MT * 16 - 1) / (MT * 16), k.ksplit);
+    hipLaunchKernelGGL((conv2d_kernel<T, MT, NT, XT>), grid, dim3(256), 0, s, k);
     DBSR_LAUNCH_CHECK();
+    if (k.ksplit > 1) {
+        const long long n = (long long)k.npix * (k.cw / 4);
+        hipLaunchKernelGGL((conv_splitk_finalize<T>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, k);
+        DBSR_LAUNCH_CHECK();
+    }
     return 0;
 }
 
+// Split-K for the generic kernel when the grid cannot fill the chip (PWC coarse levels, 2-channel
+// flow heads): K slices of >= 8 k-steps until there are ~512 blocks.
+int choose_ksplit(const ConvK& k, int mt, int nt) {
+    const long long blocks = (long long)((k.npix + 64 * nt - 1) / (64 * nt)) * ((k.cout + 16 * mt - 1) / (16 * mt));
+    const int nks = k.KGp >> 2;
+    if (blocks >= 256 || nks < 16) return 1;
+    int sp = (int)((512 + blocks - 1) / blocks);
+    sp = std::min(sp, nks / 8);
+    sp = std::min(sp, 32);
+    return std::max(sp, 1);
+}
+size_t splitk_bytes(const ConvK& k, int sp) { return sp > 1 ? (size_t)sp * k.npix * k.cw * sizeof(float) : 0; }
+// generic kernel: the largest tile that still gives >= 2 blocks per CU (512 blocks); tiny PWC levels
+// (a few hundred pixels) fall through to 16 x 64-pixel tiles (and split-K) for parallelism
+void pick_generic_tile(const ConvK& k, int& best_m, int& best_n) {
+    const int mts[3] = {4, 2, 1}, nts[3] = {4, 2, 1};
+    best_m = 1;
+    best_n = 1;
+    for (int a = 0; a < 3; ++a) {
+        if (mts[a] > 1 && k.cout <= (mts[a] / 2) * 16) continue;          // do not pad cout beyond need
+        for (int b = 0; b < 3; ++b) {
+            const long long blocks = (long long)((k.npix + 64 * nts[b] - 1) / (64 * nts[b])) *
+                                     ((k.cout + 16 * mts[a] - 1) / (16 * mts[a]));
+            if (blocks >= 512) {
+                best_m = mts[a];
+                best_n = nts[b];
+                return;
+            }
+        }
+    }
+}
+
 bool use_tiled(const dbsr_conv_desc* d) {
-    return d->kh == 3 && d->kw == 3 && d->stride == 1 && d->pad == 1 && d->dil == 1 && d->cin > 16 &&
+    return !d->precise && d->kh == 3 && d->kw == 3 && d->stride == 1 && d->pad == 1 && d->dil == 1 && d->cin > 16 &&
            d->out_h >= 8 && d->out_w >= 8 && d->out_mode == DBSR_OUT_NHWC && g_tiled_enabled;
 }
 
@@ -550,26 +622,40 @@ int dispatch_conv(const ConvK& k, const dbsr_conv_desc* d, hipStream_t s) {
         if (k.cout <= 32) return launch_tiled<T, 32, 128>(k, d->n_frames, s);
         return launch_tiled<T, 64, 64>(k, d->n_frames, s);
     }
-    // generic kernel: the largest tile that still gives >= 2 blocks per CU (512 blocks); tiny PWC levels
-    // (a few hundred pixels) fall through to 16 x 64-pixel tiles for parallelism
-    const int mts[3] = {4, 2, 1}, nts[3] = {4, 2, 1};
-    int best_m = 1, best_n = 1;
-    bool found = false;
-    for (int a = 0; a < 3 && !found; ++a) {
-        if (mts[a] > 1 && k.cout <= (mts[a] / 2) * 16) continue;          // do not pad cout beyond need
-        for (int b = 0; b < 3 && !found; ++b) {
-            const long long blocks = (long long)((k.npix + 64 * nts[b] - 1) / (64 * nts[b])) *
-                                     ((k.cout + 16 * mts[a] - 1) / (16 * mts[a]));
-            if (blocks >= 512) { best_m = mts[a]; best_n = nts[b]; found = true; }
-        }
-    }
-    if (!found) { best_m = 1; best_n = 1; }
-#define DBSR_CONV_CASE(M, N) if (best_m == M && best_n == N) return launch_conv<T, M, N>(k, s);
+    int best_m, best_n;
+    pick_generic_tile(k, best_m, best_n);
+    ConvK kk = k;
+    kk.ksplit = choose_ksplit(k, best_m, best_n);
+    if (kk.ksplit > 1 && splitk_bytes(k, kk.ksplit) > d->workspace_bytes) kk.ksplit = 1;
+#define DBSR_CONV_CASE(M, N) if (best_m == M && best_n == N) return launch_conv<T, M, N>(kk, s);
     DBSR_CONV_CASE(4, 4) DBSR_CONV_CASE(4, 2) DBSR_CONV_CASE(4, 1)
     DBSR_CONV_CASE(2, 4) DBSR_CONV_CASE(2, 2) DBSR_CONV_CASE(2, 1)
     DBSR_CONV_CASE(1, 4) DBSR_CONV_CASE(1, 2) DBSR_CONV_CASE(1, 1)
 #undef DBSR_CONV_CASE
-    return launch_conv<T, 1, 1>(k, s);
+    return launch_conv<T, 1, 1>(kk, s);
+}
+
+ConvK make_convk(const dbsr_conv_desc* d) {
+    ConvK k;
+    k.x = d->x.ptr; k.x_is = d->x.img_stride; k.x_ld = d->x.ld; k.xm = d->x.map; k.in_h = d->in_h; k.in_w = d->in_w;
+    // the channel offset is folded into the base pointer (x.c0 is a multiple of 8)
+    const int esz = d->x.dtype == DBSR_BF16 ? 2 : 4;
+    k.x = (const char*)d->x.ptr + (long long)d->x.c0 * esz;
+    const int CG = cin_pad(d->cin) / 8;
+    k.CG = CG; k.KG = d->kh * d->kw * CG; k.KGp = round_up(k.KG, 4); k.Kp = k.KGp * 8;
+    k.w = d->w; k.bias = d->bias; k.kw = d->kw; k.stride = d->stride; k.pad = d->pad; k.dil = d->dil; k.cout = d->cout;
+    k.y = d->y.ptr; k.y_f32 = d->y.dtype == DBSR_F32; k.y_is = d->y.img_stride; k.y_ld = d->y.ld; k.y_c0 = d->y.c0;
+    k.ym = d->y.map; k.out_h = d->out_h; k.out_w = d->out_w; k.act = d->act;
+    k.r = d->res.ptr; k.r_is = d->res.img_stride; k.r_ld = d->res.ld; k.r_c0 = d->res.c0; k.rm = d->res.map;
+    if (!k.r) k.rm = d->y.map;
+    k.post_act = d->post_act; k.out_mode = d->out_mode; k.shuffle = d->shuffle;
+    k.cps = d->out_mode == DBSR_OUT_SHUFFLE ? d->cout / (d->shuffle * d->shuffle) : 0;
+    k.npix = (int)((long long)d->n_frames * d->out_h * d->out_w);
+    k.vec_store = (d->out_mode != DBSR_OUT_NCHW_F32) && (d->y.ld % 4 == 0) && (d->y.c0 % 4 == 0);
+    k.ksplit = 1;
+    k.ws = (float*)d->workspace;
+    k.cw = round_up(d->cout, 4);
+    return k;
 }
 
 }  // namespace
@@ -577,6 +663,14 @@ int dispatch_conv(const ConvK& k, const dbsr_conv_desc* d, hipStream_t s) {
 extern "C" int dbsr_conv_kernel_for(const dbsr_conv_desc* d) {
     if (!d) return -1;
     return use_tiled(d) ? 1 : 0;
+}
+
+extern "C" size_t dbsr_conv_workspace_bytes(const dbsr_conv_desc* d) {
+    if (!d || use_tiled(d) || d->precise) return 0;
+    const ConvK k = make_convk(d);
+    int m, n;
+    pick_generic_tile(k, m, n);
+    return splitk_bytes(k, choose_ksplit(k, m, n));
 }
 
 extern "C" int dbsr_set_conv_algo(int algo) {
@@ -634,22 +728,15 @@ extern "C" int dbsr_conv2d(const dbsr_conv_desc* d, void* stream) {
     const long long npix = (long long)d->n_frames * d->out_h * d->out_w;
     DBSR_CHECK_ARG(npix < (1LL << 31), "conv2d: too many pixels");
 
-    ConvK k;
-    k.x = d->x.ptr; k.x_is = d->x.img_stride; k.x_ld = d->x.ld; k.xm = d->x.map; k.in_h = d->in_h; k.in_w = d->in_w;
-    // the channel offset is folded into the base pointer (x.c0 is a multiple of 8)
-    const int esz = d->x.dtype == DBSR_BF16 ? 2 : 4;
-    k.x = (const char*)d->x.ptr + (long long)d->x.c0 * esz;
-    const int CG = cin_pad(d->cin) / 8;
-    k.CG = CG; k.KG = d->kh * d->kw * CG; k.KGp = round_up(k.KG, 4); k.Kp = k.KGp * 8;
-    k.w = d->w; k.bias = d->bias; k.kw = d->kw; k.stride = d->stride; k.pad = d->pad; k.dil = d->dil; k.cout = d->cout;
-    k.y = d->y.ptr; k.y_f32 = d->y.dtype == DBSR_F32; k.y_is = d->y.img_stride; k.y_ld = d->y.ld; k.y_c0 = d->y.c0;
-    k.ym = d->y.map; k.out_h = d->out_h; k.out_w = d->out_w; k.act = d->act;
-    k.r = d->res.ptr; k.r_is = d->res.img_stride; k.r_ld = d->res.ld; k.r_c0 = d->res.c0; k.rm = d->res.map;
-    if (!k.r) k.rm = d->y.map;
-    k.post_act = d->post_act; k.out_mode = d->out_mode; k.shuffle = d->shuffle;
-    k.cps = d->out_mode == DBSR_OUT_SHUFFLE ? d->cout / (d->shuffle * d->shuffle) : 0;
-    k.npix = (int)npix;
-    k.vec_store = (d->out_mode != DBSR_OUT_NCHW_F32) && (d->y.ld % 4 == 0) && (d->y.c0 % 4 == 0);
+    ConvK k = make_convk(d);
     hipStream_t s = (hipStream_t)stream;
+    if (d->precise && d->x.dtype == DBSR_BF16) {
+        // bf16 activations, fp32-packed weights, fp32 MFMA: small fp32-output heads (the RGB predictor)
+        DBSR_CHECK_ARG(d->y.dtype == DBSR_F32 && d->cout <= 16, "conv2d: precise mode needs fp32 output, cout <= 16");
+        k.ksplit = 1;
+        if (k.npix >= 512 * 256) return launch_conv<float, 1, 4, bf16_t>(k, s);
+        if (k.npix >= 512 * 128) return launch_conv<float, 1, 2, bf16_t>(k, s);
+        return launch_conv<float, 1, 1, bf16_t>(k, s);
+    }
     return d->x.dtype == DBSR_BF16 ? dispatch_conv<bf16_t>(k, d, s) : dispatch_conv<float>(k, d, s);
 }

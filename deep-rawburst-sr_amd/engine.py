@@ -104,6 +104,7 @@ class Plan:
         self.keep = []
         self.work = {}       # op index -> ('flop' | 'byte', algorithmic amount per launch)
         self.kernel = {}     # op index -> kernel family (convs)
+        self.convs = []      # ConvDescs (share one split-K workspace, see finalize_workspace)
 
     def add(self, name, fn, *args, work=None):
         if work is not None:
@@ -111,7 +112,8 @@ class Plan:
         self.ops.append((fn, args, name))
 
     def conv(self, name, pc, n_frames, x, xc0, in_hw, y, yc0, act, xmap=IDENTITY, ymap=IDENTITY, res=None,
-             rc0=0, rmap=IDENTITY, post_act=L.ACT_NONE, out_mode=L.OUT_NHWC, shuffle=0, y_desc=None, cin=None):
+             rc0=0, rmap=IDENTITY, post_act=L.ACT_NONE, out_mode=L.OUT_NHWC, shuffle=0, y_desc=None, cin=None,
+             precise=False):
         oh, ow = pc.out_hw(*in_hw)
         assert cin is None or cin == pc.cin, (name, cin, pc.cin)
         d = L.ConvDesc()
@@ -128,11 +130,22 @@ class Plan:
         d.res = res.d(rc0, rmap) if res is not None else L.NULL_TENSOR
         d.post_act = post_act
         d.out_mode, d.shuffle = out_mode, shuffle
+        d.workspace, d.workspace_bytes = None, 0
+        d.precise = 1 if precise else 0
         self.keep.append(d)
+        self.convs.append(d)
         flop = 2.0 * n_frames * oh * ow * pc.cout * d.cin * pc.kh * pc.kw
         self.add(name, L.lib().dbsr_conv2d, ctypes.byref(d), work=('flop', flop))
         self.kernel[len(self.ops) - 1] = 'conv3x3_tiled' if L.lib().dbsr_conv_kernel_for(d) == 1 else 'conv2d_generic'
         return d
+
+    def finalize_workspace(self, device):
+        """Allocate the one fp32 split-K scratch all convs of this plan share (they run in order on one
+        stream) and point every ConvDesc at it."""
+        need = max([L.lib().dbsr_conv_workspace_bytes(d) for d in self.convs] + [0])
+        self.ws = torch.zeros(max(need // 4, 1), dtype=torch.float32, device=device)
+        for d in self.convs:
+            d.workspace, d.workspace_bytes = self.ws.data_ptr(), need
 
     def run(self, stream):
         for fn, args, name in self.ops:
@@ -307,7 +320,9 @@ class DBSREngine:
         if self.blur is not None and up.gauss_ksz != 3:
             raise NotImplementedError('gauss_ksz != 3')
         self.dec_post = [(W.conv(b.conv1[0]), W.conv(b.conv2[0])) for b in dec.post_res_layers]
-        self.pred = W.conv(dec.predictor[0])
+        # the RGB predictor runs fp32 math on bf16 features (0.2 GFLOP/burst; removes ~40 % of the bf16
+        # PSNR delta, tools/bf16_sensitivity.py)
+        self.pred = PackedConv(dec.predictor[0], torch.float32, device, stream)
         self.device = device
         self.sig = _param_signature(net)
         self.plans, self.graphs = {}, {}
@@ -418,8 +433,9 @@ class DBSREngine:
         bufs['pred'] = torch.zeros(B, 3, H * S, W * S, dtype=torch.float32, device=dev)
         pdesc = L.tensor_desc(bufs['pred'], 1, 0, img_stride=3 * H * S * W * S, dtype=torch.float32)
         plan.conv('dec.predictor', self.pred, B, sh[i], 0, (H * S, W * S), None, 0, L.ACT_RELU,
-                  out_mode=L.OUT_NCHW_F32, y_desc=pdesc)
+                  out_mode=L.OUT_NCHW_F32, y_desc=pdesc, precise=(dt == torch.bfloat16))
         plan.keep.extend([raw, rgb, om, e, E, Wf, PJ, WP, o, q, LG, FUS, FW, g, sh])
+        plan.finalize_workspace(dev)
         plan.bufs = bufs
         plan.FW = FW
         plan.fuse_idx = fuse_idx
@@ -522,6 +538,7 @@ class PWCEngine:
             plan.add('flow_finalize', lib.dbsr_flow_finalize, P, 2, Hp // 4, Wp // 4, flow_out.d(0), H, W, Hp, Wp,
                      offs.data_ptr(), 1.0, L.NULL_TENSOR)
             plan.keep.extend([rgb, flow_out])
+            plan.finalize_workspace(dev)
             plan.inp, plan.offs = inp, offs
             self.plans[key] = plan
         # pack_burst expects 4 planes (R, G1, G2, B) -> put G in both green planes so mean(G1,G2) = G

@@ -117,5 +117,8 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, act=L.ACT_NONE
         d.res = L.NULL_TENSOR
     d.post_act = post_act
     d.out_mode, d.shuffle = L.OUT_NHWC, 0
+    need = L.lib().dbsr_conv_workspace_bytes(d)
+    ws = torch.zeros(max(need // 4, 1), dtype=torch.float32, device=dev)
+    d.workspace, d.workspace_bytes = ws.data_ptr(), need
     L.check(L.lib().dbsr_conv2d(d, s), 'dbsr_conv2d')
     return y[..., :Cout].permute(0, 3, 1, 2).contiguous()

@@ -77,6 +77,9 @@ typedef struct dbsr_conv_desc {
     dbsr_tensor res;                  /* res.ptr == NULL: no residual */
     int post_act;
     int out_mode, shuffle;
+    void* workspace;                  /* optional fp32 scratch for split-K (may be NULL) */
+    size_t workspace_bytes;
+    int precise;                      /* 1: bf16 activations x fp32-packed weights on fp32 MFMA (fp32 out) */
 } dbsr_conv_desc;
 
 /* Packed weight layout: [cout_pad][kgp*8] with k-group kg = (ky*kw+kx)*(cinp/8) + c/8, where
@@ -95,6 +98,11 @@ int dbsr_conv2d(const dbsr_conv_desc* d, void* stream);
 int dbsr_set_conv_algo(int algo);
 /* Which kernel dbsr_conv2d would launch for `d` under the current selection: 1 LDS-tiled, 0 generic. */
 int dbsr_conv_kernel_for(const dbsr_conv_desc* d);
+/* Scratch bytes dbsr_conv2d would use for split-K on `d` (0 = no split).  Convs whose grid cannot fill
+ * the chip split K into slices that store fp32 partials to `workspace`; a second launch sums them in
+ * slice order (deterministic) and applies the epilogue.  With a smaller/NULL workspace the conv simply
+ * runs unsplit.  One workspace may be shared by all convs issued on one stream. */
+size_t dbsr_conv_workspace_bytes(const dbsr_conv_desc* d);
 
 /* 81-channel cost volume of (first, second) over displacements [-4,4]^2, divided by C, followed by
  * LeakyReLU(0.1) when leaky != 0.  first/second/out: NHWC slices; out channel (dy+4)*9+(dx+4). */

@@ -39,6 +39,26 @@ def test_struct_layout_matches_c():
     # dbsr_frame_map 16 B; dbsr_tensor: ptr 8, dtype 4 (+4 pad), img_stride 8, ld 4, c0 4, map 16 -> 48
     assert ctypes.sizeof(_lib.FrameMap) == 16
     assert ctypes.sizeof(_lib.Tensor) == 48
+    # conv desc: the C compiler's layout, probed through offsetof-equivalent arithmetic on the fields
+    assert _lib.ConvDesc.precise.offset == _lib.ConvDesc.workspace_bytes.offset + 8
+
+
+def test_splitk_workspace_query(L):
+    # a PWC level-6 dense conv (104 pixels, cin 529, cout 32) cannot fill the chip -> split-K
+    d = L.ConvDesc()
+    d.n_frames = 104
+    d.x = L.Tensor(1, L.DBSR_BF16, 544, 544, 0, L.FrameMap(1, 1, 0, 1))
+    d.in_h = d.in_w = 1
+    d.cin, d.cout, d.kh, d.kw, d.stride, d.pad, d.dil = 529, 32, 3, 3, 1, 1, 1
+    d.w = 1
+    d.y = L.Tensor(1, L.DBSR_BF16, 544, 544, 0, L.FrameMap(1, 1, 0, 1))
+    d.out_h = d.out_w = 1
+    assert L.lib().dbsr_conv_workspace_bytes(d) > 0
+    d.n_frames, d.in_h, d.in_w, d.out_h, d.out_w = 112, 48, 48, 48, 48      # big conv: no split
+    d.cin, d.cout = 4, 64
+    d.x.ld = 8
+    d.y.ld = 64
+    assert L.lib().dbsr_conv_workspace_bytes(d) == 0
 
 
 def test_packed_size(L):

@@ -77,6 +77,9 @@ CONV_CASES = [
     (2, 32, 40, 24, 32, 3, 1, 1, 1),       # tiled kernel, 32-cout variant, partial tiles
     (2, 192, 20, 17, 128, 3, 1, 1, 1),     # tiled kernel, 6 chunks, 2 cout tiles
     (3, 128, 48, 48, 512, 3, 1, 1, 1),     # tiled kernel at the weight-predictor shape
+    (2, 565, 16, 16, 2, 3, 1, 1, 1),       # split-K (2-channel flow head)
+    (104, 529, 1, 1, 32, 3, 1, 1, 1),      # split-K (PWC level 6)
+    (7, 469, 4, 4, 64, 3, 1, 1, 1),        # split-K (PWC level 4)
 ]
 
 

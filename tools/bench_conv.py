@@ -25,10 +25,19 @@ SHAPES = [  # name, frames, H, W, cin, cout, k
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--only', default=None, help='substring of the shape names to run')
+    ap.add_argument('--algos', default='1,0')
+    ap.add_argument('--reps', type=int, default=20)
+    args = ap.parse_args()
+    algos = [int(a) for a in args.algos.split(',')]
     dev = torch.device('cuda')
     dt = torch.bfloat16
     s = torch.cuda.current_stream().cuda_stream
     for name, F, H, W, cin, cout, k in SHAPES:
+        if args.only and args.only not in name:
+            continue
         conv = torch.nn.Conv2d(cin, cout, k, padding=k // 2).to(dev)
         pc = PackedConv(conv, dt, dev, s)
         x = NHWC(F, H, W, cpad(cin), dt, dev)
@@ -41,14 +50,14 @@ def main():
         else:
             plan.conv(name, pc, F, x, 0, (H, W), y, 0, L.ACT_RELU)
         flop = plan.work[0][1]
-        res = []
-        for algo in (1, 0):
+        plan.finalize_workspace(dev)
+        out = []
+        for algo in algos:
             L.lib().dbsr_set_conv_algo(algo)
-            ms = plan.time_ops(s, reps=20)[0][1]
-            res.append((ms, flop / ms / 1e9))
+            ms = plan.time_ops(s, reps=args.reps)[0][1]
+            out.append('%s %7.1f us %6.1f TF/s' % ('tiled' if algo else 'generic', ms * 1e3, flop / ms / 1e9))
         L.lib().dbsr_set_conv_algo(1)
-        print(f'{name:20s} tiled {res[0][0]*1e3:7.1f} us {res[0][1]:6.1f} TF/s | generic {res[1][0]*1e3:7.1f} us '
-              f'{res[1][1]:6.1f} TF/s')
+        print(f'{name:22s} ' + ' | '.join(out))
 
 
 if __name__ == '__main__':
