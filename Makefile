@@ -23,7 +23,16 @@ $(OBJDIR)/%.o: $(SRC)/%.cpp include/dbsr_hip.h
 $(LIB): $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
 
-clean:
-	rm -rf $(OBJDIR) $(LIB)
+# Experiment build: same sources with extra -D flags, loaded via DBSR_HIP_LIB for A/B profiling.
+EXP_FLAGS ?=
+EXP_LIB   := $(PKG)/libdbsr_hip_exp.so
+exp:
+	@mkdir -p $(OBJDIR)/exp
+	for f in $(HIPSRCS) $(CPPSRCS); do \
+	  $(HIPCC) $(FLAGS) $(EXP_FLAGS) -c $$f -o $(OBJDIR)/exp/$$(basename $$f).o || exit 1; done
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(EXP_LIB) $(OBJDIR)/exp/*.o
 
-.PHONY: all clean
+clean:
+	rm -rf $(OBJDIR) $(LIB) $(EXP_LIB)
+
+.PHONY: all clean exp

@@ -13,13 +13,15 @@ typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
 
 __device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((unsigned)v) << 16); }
 
-// round-to-nearest-even; NaN kept NaN (MI355X_MICROARCH.md correctness table: plain cast path)
-__device__ __forceinline__ bf16_t f2bf(float f) {
-    unsigned u = __float_as_uint(f);
-    if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) return (bf16_t)((u >> 16) | 0x40);
-    u += 0x7fffu + ((u >> 16) & 1u);
-    return (bf16_t)(u >> 16);
+// fp32 -> bf16, round-to-nearest-even, NaN kept NaN: the plain cast lowers to the hardware
+// v_cvt_pk_bf16_f32 (MI355X_MICROARCH.md correctness table), one VALU op per two values instead of
+// the ~7-op integer rounding sequence (which made the warp kernel VALU-bound)
+typedef __attribute__((ext_vector_type(2))) float f32x2_t;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+__device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {
+    return __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2_t{lo, hi}, bf16x2_t));
 }
+__device__ __forceinline__ bf16_t f2bf(float f) { return __builtin_bit_cast(unsigned short, (__bf16)f); }
 
 template <typename T> struct elem;
 template <> struct elem<float> {
@@ -51,7 +53,7 @@ __device__ __forceinline__ void store8(float* p, const float (&v)[8]) {
 __device__ __forceinline__ void store8(bf16_t* p, const float (&v)[8]) {
     u32x4_t q;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) q[i] = (unsigned)f2bf(v[2 * i]) | ((unsigned)f2bf(v[2 * i + 1]) << 16);
+    for (int i = 0; i < 4; ++i) q[i] = pack_bf16x2(v[2 * i], v[2 * i + 1]);
     *(u32x4_t*)p = q;
 }
 

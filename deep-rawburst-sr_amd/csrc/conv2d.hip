@@ -109,8 +109,8 @@ __device__ __forceinline__ void store4(const ConvK& k, long long off, const floa
         if (nvalid == 4 && k.vec_store) {
             if constexpr (sizeof(T) == 2) {
                 uint2 q;
-                q.x = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
-                q.y = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
+                q.x = pack_bf16x2(v[0], v[1]);
+                q.y = pack_bf16x2(v[2], v[3]);
                 *(uint2*)y = q;
             } else {
                 *(float4*)y = make_float4(v[0], v[1], v[2], v[3]);
@@ -325,8 +325,10 @@ struct TileCfg {
     static constexpr int OSTR = WM * (int)sizeof(T) + 16;     // staged-output pixel stride (bytes)
 };
 
-// 16 zero bytes per lane for halo pixels outside the frame (LDS-DMA cannot write zeros itself)
-__device__ __attribute__((aligned(16))) u32x4_t g_dbsr_zero16[64];
+// zero page for halo pixels outside the frame (LDS-DMA cannot write zeros itself); those lanes' source
+// pointers advance by the chunk offset like every other lane, so the page covers 32 KiB of chunks
+constexpr int ZERO_PAGE_BYTES = 32768;
+__device__ __attribute__((aligned(16))) u32x4_t g_dbsr_zero16[ZERO_PAGE_BYTES / 16];
 
 __device__ __forceinline__ void glds16(const void* src, u32x4_t* lds_piece) {
     __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_piece, 16, 0, 0);
@@ -369,25 +371,47 @@ __global__ __launch_bounds__(256, 2) void conv3x3_tiled_kernel(ConvK k, int tile
     //        reads are 16 distinct bank slots for every tap shift (conflict-free), and a pixel's
     //        address is linear in the tap shift (immediate-offset reads).
     //  weights: one piece = 16 output channels x 4 k-groups of one tap (16 x 64 contiguous bytes).
+    // Per-lane source pointers of every piece this wave stages, computed once per block: a chunk only
+    // adds chunk * 32 elements (the address math is otherwise VALU work on every chunk).
+    constexpr int IN_PER = (C::IN_ITEMS + 3) / 4, W_PER = (C::W_ITEMS + 3) / 4;
+    const char* in_src[IN_PER];
+    const char* w_src[W_PER];
+#pragma unroll
+    for (int it = 0; it < IN_PER; ++it) {
+        const int item = wave + 4 * it;
+        const int plane = item / (C::NQP / 64), seg = item % (C::NQP / 64);
+        const int gg = plane / C::HALVES, h = plane % C::HALVES;
+        const int q = seg * 64 + lane;
+        const char* src = (const char*)g_dbsr_zero16;
+        if (item < C::IN_ITEMS && q < C::NQ) {
+            const int iy = y0 - 1 + q / C::HWD, ix = x0 - 1 + q % C::HWD;
+            if ((unsigned)iy < (unsigned)k.in_h && (unsigned)ix < (unsigned)k.in_w)
+                src = (const char*)(xf + ((long long)iy * k.in_w + ix) * k.x_ld + gg * 8 + h * 4);
+        }
+        in_src[it] = src;
+    }
+#pragma unroll
+    for (int it = 0; it < W_PER; ++it) {
+        const int item = wave + 4 * it;
+        const int h = item % C::HALVES, rest = item / C::HALVES;
+        const int cb = rest % (WM / 16), tap = rest / (WM / 16);
+        const int co = c_base + cb * 16 + col;
+        w_src[it] = (const char*)((const T*)k.w + (long long)co * k.Kp + (tap * k.CG + g) * 8 + h * 4);
+    }
+    // Stage one 32-channel chunk by LDS-DMA (16 B per lane, lane-linear destination):
+    //  halo: one piece = 64 consecutive pixels of one (k-group, half) plane; pixels outside the frame
+    //        read the zero page.  Planes are 1-KiB multiples, so the 16 pixels a ds_read_b128 lane group
+    //        reads are 16 distinct bank slots for every tap shift (conflict-free), and a pixel's
+    //        address is linear in the tap shift (immediate-offset reads).
+    //  weights: one piece = 16 output channels x 4 k-groups of one tap (16 x 64 contiguous bytes).
     auto issue = [&](int chunk) {
-        for (int item = wave; item < C::IN_ITEMS; item += 4) {
-            const int plane = item / (C::NQP / 64), seg = item % (C::NQP / 64);
-            const int gg = plane / C::HALVES, h = plane % C::HALVES;
-            const int q = seg * 64 + lane;
-            const void* src = g_dbsr_zero16;
-            if (q < C::NQ) {
-                const int iy = y0 - 1 + q / C::HWD, ix = x0 - 1 + q % C::HWD;
-                if ((unsigned)iy < (unsigned)k.in_h && (unsigned)ix < (unsigned)k.in_w)
-                    src = xf + ((long long)iy * k.in_w + ix) * k.x_ld + chunk * 32 + gg * 8 + h * 4;
-            }
-            glds16(src, lin + item * 64);
-        }
-        for (int item = wave; item < C::W_ITEMS; item += 4) {
-            const int h = item % C::HALVES, rest = item / C::HALVES;
-            const int cb = rest % (WM / 16), tap = rest / (WM / 16);
-            const int co = c_base + cb * 16 + col;
-            glds16((const T*)k.w + (long long)co * k.Kp + (tap * k.CG + chunk * 4 + g) * 8 + h * 4, lw + item * 64);
-        }
+        const int off = chunk * 32 * (int)sizeof(T);
+#pragma unroll
+        for (int it = 0; it < IN_PER; ++it)
+            if (wave + 4 * it < C::IN_ITEMS) glds16(in_src[it] + off, lin + (wave + 4 * it) * 64);
+#pragma unroll
+        for (int it = 0; it < W_PER; ++it)
+            if (wave + 4 * it < C::W_ITEMS) glds16(w_src[it] + off, lw + (wave + 4 * it) * 64);
     };
 
     f32x4_t acc[WM / 16][WN / 16];
@@ -465,8 +489,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_tiled_kernel(ConvK k, int tile
                 for (int r = 0; r < 4; ++r) v[r] = apply_act(acc[i][j][r] + bias[i][r], k.act);
                 if constexpr (sizeof(T) == 2) {
                     uint2 q;
-                    q.x = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
-                    q.y = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
+                    q.x = pack_bf16x2(v[0], v[1]);
+                    q.y = pack_bf16x2(v[2], v[3]);
                     *(uint2*)(ob + pix * C::OSTR + co * 2) = q;
                 } else {
                     *(float4*)(ob + pix * C::OSTR + co * 4) = make_float4(v[0], v[1], v[2], v[3]);
@@ -511,8 +535,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_tiled_kernel(ConvK k, int tile
                     for (int q = 0; q < 4; ++q) {
                         const float lo = __uint_as_float(val[q] << 16) + __uint_as_float(rv[e][q] << 16);
                         const float hi = __uint_as_float(val[q] & 0xffff0000u) + __uint_as_float(rv[e][q] & 0xffff0000u);
-                        val[q] = (unsigned)f2bf(apply_act(lo, k.post_act)) |
-                                 ((unsigned)f2bf(apply_act(hi, k.post_act)) << 16);
+                        val[q] = pack_bf16x2(apply_act(lo, k.post_act), apply_act(hi, k.post_act));
                     }
                 } else {
 #pragma unroll
@@ -612,7 +635,7 @@ void pick_generic_tile(const ConvK& k, int& best_m, int& best_n) {
 }
 
 bool use_tiled(const dbsr_conv_desc* d) {
-    return !d->precise && d->kh == 3 && d->kw == 3 && d->stride == 1 && d->pad == 1 && d->dil == 1 && d->cin > 16 &&
+    return !d->precise && cin_pad(d->cin) * (d->x.dtype == DBSR_BF16 ? 2 : 4) + 64 <= ZERO_PAGE_BYTES && d->kh == 3 && d->kw == 3 && d->stride == 1 && d->pad == 1 && d->dil == 1 && d->cin > 16 &&
            d->out_h >= 8 && d->out_w >= 8 && d->out_mode == DBSR_OUT_NHWC && g_tiled_enabled;
 }
 
