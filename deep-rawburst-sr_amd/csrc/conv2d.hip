@@ -607,8 +607,10 @@ int launch_conv(const ConvK& k, hipStream_t s) {
 int choose_ksplit(const ConvK& k, int mt, int nt) {
     const long long blocks = (long long)((k.npix + 64 * nt - 1) / (64 * nt)) * ((k.cout + 16 * mt - 1) / (16 * mt));
     const int nks = k.KGp >> 2;
-    if (blocks >= 256 || nks < 16) return 1;
-    int sp = (int)((512 + blocks - 1) / blocks);
+    // long-K convs (the 2-channel flow heads: K = 9 x 565) also split while the grid is < 4 blocks/CU
+    const long long target = nks >= 64 ? 1024 : 512;
+    if (blocks >= target / 2 || nks < 16) return 1;
+    int sp = (int)((target + blocks - 1) / blocks);
     sp = std::min(sp, nks / 8);
     sp = std::min(sp, 32);
     return std::max(sp, 1);
@@ -642,7 +644,10 @@ bool use_tiled(const dbsr_conv_desc* d) {
 template <typename T>
 int dispatch_conv(const ConvK& k, const dbsr_conv_desc* d, hipStream_t s) {
     if (use_tiled(d)) {
-        if (k.cout <= 32) return launch_tiled<T, 32, 128>(k, d->n_frames, s);
+        if (k.cout <= 32) {
+            if (d->out_h >= 32) return launch_tiled<T, 32, 128>(k, d->n_frames, s);   // 32x16 tiles
+            return launch_tiled<T, 32, 64>(k, d->n_frames, s);                       // 16x16 tiles
+        }
         return launch_tiled<T, 64, 64>(k, d->n_frames, s);
     }
     int best_m, best_n;

@@ -88,6 +88,75 @@ __global__ __launch_bounds__(256) void warp_kernel(int n, int h, int w, int grou
     }
 }
 
+// C == 512 (64 lanes x 8 channels = one pixel per wave-row): each wave handles PPW consecutive
+// pixels, issues all 4*PPW tap loads before consuming any (the per-pixel version had two dependent
+// memory round trips and only 4 KiB in flight per wave: latency-bound), and reads the flow with
+// wave-uniform (scalar) loads.
+template <int PPW>
+__global__ __launch_bounds__(256) void warp512_bf16_kernel(int n, int h, int w, dbsr_tensor feat,
+                                                           const float* __restrict__ flow, long long fis,
+                                                           dbsr_tensor out) {
+    const unsigned b = blockIdx.x, nb = gridDim.x, xcd = b & 7, q8 = nb >> 3, r8 = nb & 7;
+    const unsigned lb = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+    const unsigned gw = __builtin_amdgcn_readfirstlane(lb * 4 + (threadIdx.x >> 6));
+    const int lane = threadIdx.x & 63;
+    const int hw = h * w;
+    const unsigned total = (unsigned)n * hw;
+    int tapoff[PPW][4];
+    float tapw[PPW][4];
+    const bf16_t* fbase[PPW];
+    bf16_t* obase[PPW];
+    bool live[PPW];
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+        const unsigned pix = gw * PPW + i;
+        live[i] = pix < total;
+        const unsigned pc = live[i] ? pix : 0;
+        const int p = (int)(pc / hw), rr = (int)(pc - (unsigned)p * hw);
+        const int y = rr / w, x = rr - y * w;
+        const float* fl = flow + (long long)p * fis + rr;
+        const float gx = ((float)x + 0.5f) + fl[0];
+        const float gy = ((float)y + 0.5f) + fl[hw];
+        const float gxn = 2.0f * gx / (float)w - 1.0f, gyn = 2.0f * gy / (float)h - 1.0f;
+        const float ix = ((gxn + 1.f) * (float)w - 1.f) / 2.f;
+        const float iy = ((gyn + 1.f) * (float)h - 1.f) / 2.f;
+        const float fx0 = floorf(ix), fy0 = floorf(iy);
+        const int x0 = (int)fx0, y0 = (int)fy0;
+        const float wx1 = ix - fx0, wx0 = 1.f - wx1, wy1 = iy - fy0, wy0 = 1.f - wy1;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int xx = x0 + (t & 1), yy = y0 + (t >> 1);
+            const bool ok = (unsigned)xx < (unsigned)w && (unsigned)yy < (unsigned)h;
+            tapw[i][t] = ok ? ((t & 1) ? wx1 : wx0) * ((t >> 1) ? wy1 : wy0) : 0.f;
+            tapoff[i][t] = ok ? (yy * w + xx) * feat.ld : 0;        // clamped: in-bounds address, weight 0
+        }
+        fbase[i] = img_ptr<bf16_t>(feat, p) + lane * 8;
+        obase[i] = img_ptr<bf16_t>(out, p) + (long long)rr * out.ld + lane * 8;
+    }
+    u32x4_t v[PPW][4];
+#pragma unroll
+    for (int i = 0; i < PPW; ++i)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) v[i][t] = *(const u32x4_t*)(fbase[i] + tapoff[i][t]);
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+        f32x2_t acc[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const f32x2_t w2 = {tapw[i][t], tapw[i][t]};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const f32x2_t x2 = {__uint_as_float(v[i][t][e] << 16), __uint_as_float(v[i][t][e] & 0xffff0000u)};
+                acc[e] = __builtin_elementwise_fma(w2, x2, acc[e]);
+            }
+        }
+        u32x4_t o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = pack_bf16x2(acc[e][0], acc[e][1]);
+        if (live[i]) *(u32x4_t*)obase[i] = o;
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 // Fusion (merging.py:116-126): w = softmax_n(logits[b,n]), fused[b] = sum_n feat[b,n] * w[b,n].
 // Thread = (b, pixel, 4 channels); the N logits stay in registers (one read of each byte), fp32
@@ -139,12 +208,21 @@ __global__ __launch_bounds__(256) void fuse_softmax_kernel(int B, int N, int hw,
         rr = (int)(pix - (long long)b * hw);
     }
     const int c = g * 4;
-    float l[NMAX][4];
+    float l[NMAX][4], fv[NMAX][4];
     float m[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    // issue every logit and feature load up front (2N independent loads in flight per thread)
 #pragma unroll
     for (int n = 0; n < NMAX; ++n) {
         if (n < N) {
             Vec4<T>::ld(img_ptr<T>(logits, b * N + n) + (long long)rr * logits.ld + c, l[n]);
+            const T* fp = n == 0 ? img_ptr<T>(ref, b) + (long long)rr * ref.ld
+                                 : img_ptr<T>(oth, b * (N - 1) + n - 1) + (long long)rr * oth.ld;
+            Vec4<T>::ld(fp + c, fv[n]);
+        }
+    }
+#pragma unroll
+    for (int n = 0; n < NMAX; ++n) {
+        if (n < N) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) m[j] = fmaxf(m[j], l[n][j]);
         }
@@ -167,14 +245,11 @@ __global__ __launch_bounds__(256) void fuse_softmax_kernel(int B, int N, int hw,
 #pragma unroll
     for (int n = 0; n < NMAX; ++n) {
         if (n < N) {
-            const T* fp = n == 0 ? img_ptr<T>(ref, b) : img_ptr<T>(oth, b * (N - 1) + n - 1);
-            const int ldf = n == 0 ? ref.ld : oth.ld;
-            float f[4], wn[4];
-            Vec4<T>::ld(fp + (long long)rr * ldf + c, f);
+            float wn[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 wn[j] = l[n][j] * inv[j];
-                acc[j] = fmaf(f[j], wn[j], acc[j]);
+                acc[j] = fmaf(fv[n][j], wn[j], acc[j]);
             }
             if (weights.ptr) {
                 if (weights.dtype == DBSR_F32)
@@ -266,7 +341,12 @@ extern "C" int dbsr_warp_bilinear(int n, int h, int w, int c, dbsr_tensor feat, 
     const int groups = c / 8;
     return by_dtype(feat.dtype, [&](auto* tag) {
         using T = std::remove_pointer_t<decltype(tag)>;
-        if (groups % 64 == 0)
+        if (sizeof(T) == 2 && groups == 64) {
+            constexpr int PPW = 4;
+            const long long waves = ((long long)n * h * w + PPW - 1) / PPW;
+            hipLaunchKernelGGL((warp512_bf16_kernel<PPW>), dim3(nblocks(waves, 4)), dim3(256), 0, (hipStream_t)stream,
+                               n, h, w, feat, flow, flow_img_stride, out);
+        } else if (groups % 64 == 0)
             hipLaunchKernelGGL((warp_kernel<T, true>), dim3(nblocks((long long)n * h * w * groups, 256)), dim3(256), 0,
                                (hipStream_t)stream, n, h, w, groups, feat, flow, flow_img_stride, out);
         else
