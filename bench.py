@@ -115,6 +115,8 @@ def main():
     value = world * B * args.steps / el
     fam = {}
     for i, (name, ms) in enumerate(times):
+        if name.startswith('sync.'):
+            continue
         kind = plan.kernel.get(i) or name.split('.')[-1]
         f = fam.setdefault(kind, [0.0, 0.0, 0])
         f[0] += ms
@@ -140,6 +142,8 @@ def main():
                       'alg_bytes': by}
     if args.kernel_breakdown and rank == 0:
         for name, ms in times:
+            if name.startswith('sync.'):
+                continue
             print(f'{name:32s} {ms * 1e3:9.1f} us', file=sys.stderr)
         for k, (ms, w, n) in sorted(fam.items(), key=lambda kv: -kv[1][0]):
             print(f'[family] {k:12s} {ms * 1e3:9.1f} us  n={n}', file=sys.stderr)

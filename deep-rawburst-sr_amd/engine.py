@@ -99,17 +99,49 @@ class PackedConv:
 
 
 class Plan:
+    """A forward as a flat list of C-ABI launches over preallocated buffers, on one or more lanes.
+
+    Lane 0 is the caller's stream; every other lane is a side stream that `fork` starts (it waits for
+    all lane-0 work issued so far) and `join` ends (lane 0 waits for it).  Independent sub-graphs (the
+    PWC-Net alignment vs the feature encoder) overlap this way, in eager mode and inside a HIP graph
+    capture alike.
+    """
+    FORK, JOIN = '__fork__', '__join__'
+
     def __init__(self):
-        self.ops = []        # (callable, args, name)
+        self.ops = []        # (callable | FORK | JOIN, args, name, lane)
         self.keep = []
         self.work = {}       # op index -> ('flop' | 'byte', algorithmic amount per launch)
         self.kernel = {}     # op index -> kernel family (convs)
-        self.convs = []      # ConvDescs (share one split-K workspace, see finalize_workspace)
+        self.convs = []      # (ConvDesc, lane): each lane shares one split-K workspace
+        self.lane = 0
+        self.lanes = {0}
+        self.streams = {}
 
     def add(self, name, fn, *args, work=None):
         if work is not None:
             self.work[len(self.ops)] = work
-        self.ops.append((fn, args, name))
+        self.ops.append((fn, args, name, self.lane))
+
+    def fork(self, lane, device, priority=0):
+        """Following ops go to side stream `lane`, ordered after everything issued so far on lane 0."""
+        assert self.lane == 0 and lane != 0
+        if lane not in self.streams:
+            self.streams[lane] = torch.cuda.Stream(device=device, priority=priority)
+        self.lanes.add(lane)
+        self.ops.append((Plan.FORK, (torch.cuda.Event(),), f'sync.fork{lane}', lane))
+        self.lane = lane
+
+    def switch(self, lane):
+        """Following ops go to `lane` (an already forked side lane, or 0), with no ordering edge."""
+        assert lane == 0 or lane in self.streams
+        self.lane = lane
+
+    def join(self, lane):
+        """Lane 0 waits for all work issued so far on side lane `lane`; following ops go to lane 0."""
+        assert lane != 0 and lane in self.streams
+        self.ops.append((Plan.JOIN, (torch.cuda.Event(),), f'sync.join{lane}', lane))
+        self.lane = 0
 
     def conv(self, name, pc, n_frames, x, xc0, in_hw, y, yc0, act, xmap=IDENTITY, ymap=IDENTITY, res=None,
              rc0=0, rmap=IDENTITY, post_act=L.ACT_NONE, out_mode=L.OUT_NHWC, shuffle=0, y_desc=None, cin=None,
@@ -133,31 +165,48 @@ class Plan:
         d.workspace, d.workspace_bytes = None, 0
         d.precise = 1 if precise else 0
         self.keep.append(d)
-        self.convs.append(d)
+        self.convs.append((d, self.lane))
         flop = 2.0 * n_frames * oh * ow * pc.cout * d.cin * pc.kh * pc.kw
         self.add(name, L.lib().dbsr_conv2d, ctypes.byref(d), work=('flop', flop))
         self.kernel[len(self.ops) - 1] = 'conv3x3_tiled' if L.lib().dbsr_conv_kernel_for(d) == 1 else 'conv2d_generic'
         return d
 
     def finalize_workspace(self, device):
-        """Allocate the one fp32 split-K scratch all convs of this plan share (they run in order on one
-        stream) and point every ConvDesc at it."""
-        need = max([L.lib().dbsr_conv_workspace_bytes(d) for d in self.convs] + [0])
-        self.ws = torch.zeros(max(need // 4, 1), dtype=torch.float32, device=device)
-        for d in self.convs:
-            d.workspace, d.workspace_bytes = self.ws.data_ptr(), need
+        """Allocate one fp32 split-K scratch per lane (the convs of a lane run in order on its stream;
+        lanes run concurrently) and point every ConvDesc at its lane's scratch."""
+        assert self.lane == 0, 'unjoined side lane'
+        self.ws = {}
+        for lane in sorted(self.lanes):
+            ds = [d for d, ln in self.convs if ln == lane]
+            need = max([L.lib().dbsr_conv_workspace_bytes(d) for d in ds] + [0])
+            self.ws[lane] = torch.zeros(max(need // 4, 1), dtype=torch.float32, device=device)
+            for d in ds:
+                d.workspace, d.workspace_bytes = self.ws[lane].data_ptr(), need
 
     def run(self, stream):
-        for fn, args, name in self.ops:
-            rc = fn(*args, stream)
-            if rc != 0:
-                L.check(rc, name)
+        main = torch.cuda.current_stream()
+        if self.streams:
+            assert main.cuda_stream == stream, 'Plan.run: lanes fork from the current stream'
+        for fn, args, name, lane in self.ops:
+            if fn is Plan.FORK:
+                args[0].record(main)
+                self.streams[lane].wait_event(args[0])
+            elif fn is Plan.JOIN:
+                args[0].record(self.streams[lane])
+                main.wait_event(args[0])
+            else:
+                rc = fn(*args, stream if lane == 0 else self.streams[lane].cuda_stream)
+                if rc != 0:
+                    L.check(rc, name)
 
     def time_ops(self, stream, reps=10):
         """Average device time (ms) of each op, each launched `reps` times back to back between two
-        HIP events on `stream` (the stream the ops run on)."""
+        HIP events on `stream` (all lanes serialised onto it; fork/join entries report 0)."""
         out = []
-        for fn, args, name in self.ops:
+        for fn, args, name, lane in self.ops:
+            if fn is Plan.FORK or fn is Plan.JOIN:
+                out.append((name, 0.0))
+                continue
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             fn(*args, stream)
             e0.record()
@@ -356,6 +405,10 @@ class DBSREngine:
         zero_flow = getattr(self.net, 'zero_flow', False)
         plan.add('pack_burst', lib.dbsr_pack_burst, B, N, H, W, bufs['burst'].data_ptr(), raw.d(0), Hp, Wp,
                  rgb.d(0) if not zero_flow else L.NULL_TENSOR)
+        # Two lanes: the alignment chain (PWC-Net -> offsets -> offset-feature extractor, many small
+        # latency-bound launches) runs on a high-priority side stream beside the per-frame encoder
+        # (large launches); they meet at the warp.
+        plan.fork(1, dev, priority=-1)
         # ---------------- alignment (PWC-Net) ----------------
         if not zero_flow:
             flow_out = NHWC(P, Hp // 4, Wp // 4, 2, torch.float32, dev)
@@ -365,27 +418,10 @@ class DBSREngine:
                      bufs['offsets'].data_ptr(), 1.0, om.d(0))
             plan.keep.append(flow_out)
         # (zero flow: offsets and om stay zero from initialisation)
-        # ---------------- encoder (encoders.py:66-72) ----------------
-        e = [NHWC(F, H, W, r8(self.enc_init.cout), dt, dev) for _ in range(3)]
-        plan.conv('enc.init', self.enc_init, F, raw, 0, hw, e[0], 0, L.ACT_RELU)
-        i = self._resblocks(plan, 'enc.res', self.enc_res, F, hw, e, 0, dt)
-        E = NHWC(F, H, W, C, dt, dev)
-        plan.conv('enc.out', self.enc_out, F, e[i], 0, hw, E, 0, L.ACT_RELU)
-        # ---------------- warp (encoders.py:80) ----------------
-        Wf = NHWC(max(P, 1), H, W, C, dt, dev)
-        es = 2 if dt == torch.bfloat16 else 4
-        if P > 0:
-            plan.add('warp', lib.dbsr_warp_bilinear, P, H, W, C, E.d(0, (N - 1, N, 1, 1)), bufs['offsets'].data_ptr(),
-                     2 * H * W, Wf.d(0), work=('byte', 2.0 * P * C * H * W * es + 8.0 * P * H * W))
-        # ---------------- merging (merging.py:61-127) ----------------
         pd = self.proj.cout
-        PJ = NHWC(F, H, W, r8(pd), dt, dev)
-        plan.conv('merge.proj_ref', self.proj, B, E, 0, hw, PJ, 0, L.ACT_RELU, xmap=(1, N, 0, 1), ymap=(1, N, 0, 1))
-        if P > 0:
-            plan.conv('merge.proj_oth', self.proj, P, Wf, 0, hw, PJ, 0, L.ACT_RELU, ymap=(N - 1, N, 1, 1))
         od = self.ofe_init.cout
         WP = NHWC(F, H, W, 2 * pd + od, dt, dev)
-        plan.add('merge.prep', lib.dbsr_merge_prep, B, N, H * W, pd, PJ.d(0), WP.d(0))
+        # offset-feature extractor (merging.py:85-87) -> WP[..., 2*pd:]
         o = [NHWC(F, H, W, od, dt, dev) for _ in range(3)]
         plan.conv('merge.ofe.init', self.ofe_init, F, om, 0, hw, o[0], 0, L.ACT_RELU)
         a = 0
@@ -402,6 +438,26 @@ class DBSREngine:
                 a = c
         if not self.ofe_res:
             raise NotImplementedError('num_offset_feat_extractor_res must be >= 1')
+        plan.switch(0)
+        # ---------------- encoder (encoders.py:66-72) ----------------
+        e = [NHWC(F, H, W, r8(self.enc_init.cout), dt, dev) for _ in range(3)]
+        plan.conv('enc.init', self.enc_init, F, raw, 0, hw, e[0], 0, L.ACT_RELU)
+        i = self._resblocks(plan, 'enc.res', self.enc_res, F, hw, e, 0, dt)
+        E = NHWC(F, H, W, C, dt, dev)
+        plan.conv('enc.out', self.enc_out, F, e[i], 0, hw, E, 0, L.ACT_RELU)
+        # ---------------- merging (merging.py:61-127) ----------------
+        PJ = NHWC(F, H, W, r8(pd), dt, dev)
+        plan.conv('merge.proj_ref', self.proj, B, E, 0, hw, PJ, 0, L.ACT_RELU, xmap=(1, N, 0, 1), ymap=(1, N, 0, 1))
+        plan.join(1)
+        # ---------------- warp (encoders.py:80) ----------------
+        Wf = NHWC(max(P, 1), H, W, C, dt, dev)
+        es = 2 if dt == torch.bfloat16 else 4
+        if P > 0:
+            plan.add('warp', lib.dbsr_warp_bilinear, P, H, W, C, E.d(0, (N - 1, N, 1, 1)), bufs['offsets'].data_ptr(),
+                     2 * H * W, Wf.d(0), work=('byte', 2.0 * P * C * H * W * es + 8.0 * P * H * W))
+        if P > 0:
+            plan.conv('merge.proj_oth', self.proj, P, Wf, 0, hw, PJ, 0, L.ACT_RELU, ymap=(N - 1, N, 1, 1))
+        plan.add('merge.prep', lib.dbsr_merge_prep, B, N, H * W, pd, PJ.d(0), WP.d(0))
         q = [NHWC(F, H, W, self.wp_init.cout, dt, dev) for _ in range(3)]
         plan.conv('merge.wp.init', self.wp_init, F, WP, 0, hw, q[0], 0, L.ACT_RELU)
         i = self._resblocks(plan, 'merge.wp.res', self.wp_res, F, hw, q, 0, dt)
@@ -444,10 +500,10 @@ class DBSREngine:
         return plan
 
     def _set_fw(self, plan, want):
-        fn, args, name = plan.ops[plan.fuse_idx]
+        fn, args, name, lane = plan.ops[plan.fuse_idx]
         args = list(plan.fuse_args)
         args[-1] = plan.bufs['fw_desc'] if want else L.NULL_TENSOR
-        plan.ops[plan.fuse_idx] = (fn, tuple(args), name)
+        plan.ops[plan.fuse_idx] = (fn, tuple(args), name, lane)
         plan.work[plan.fuse_idx] = ('byte', plan.fuse_bytes[0] + (plan.fuse_bytes[1] if want else 0.0))
 
     def forward(self, burst):
