@@ -311,9 +311,9 @@ __global__ void pack_weights_kernel(const float* __restrict__ w, const float* __
 // Blocks are ordered so each XCD gets a contiguous range of (tile, cout-tile) pairs: the 8 cout
 // tiles of a spatial tile and neighbouring tiles (shared halos) hit the same L2.
 // ------------------------------------------------------------------------------------------------
-template <typename T, int WM, int WN>
+template <typename T, int WM, int WN, int D>
 struct TileCfg {
-    static constexpr int TW = 16, TH = 4 * WN / 16, HWD = TW + 2, HHT = TH + 2;
+    static constexpr int TW = 16, TH = 4 * WN / 16, HWD = TW + 2 * D, HHT = TH + 2 * D;
     static constexpr int NQ = HHT * HWD;                      // halo pixels
     static constexpr int NQP = (NQ + 63) / 64 * 64;           // plane length (pixels): whole 1-KiB pieces
     static constexpr int HALVES = sizeof(T) / 2;              // 16-B halves per k-group (bf16 1, f32 2)
@@ -334,10 +334,11 @@ __device__ __forceinline__ void glds16(const void* src, u32x4_t* lds_piece) {
     __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_piece, 16, 0, 0);
 }
 
-template <typename T, int WM, int WN>
+template <typename T, int WM, int WN, int D>
 __global__ __launch_bounds__(256, 2) void conv3x3_tiled_kernel(ConvK k, int tiles_x, int tiles_y, int nct,
                                                                int nblocks) {
-    using C = TileCfg<T, WM, WN>;
+    using C = TileCfg<T, WM, WN, D>;
+    static_assert((C::IN_U4 + C::W_U4) * 16 <= 160 * 1024, "LDS tile exceeds 160 KiB");
     static_assert(C::NPIX * C::OSTR <= (C::IN_U4 + C::W_U4) * 16, "output staging must fit the LDS tile");
     // One LDS array (a second __shared__ object can de-pipeline LDS-DMA: cdna_hip_programming.md §5 item 4a)
     __shared__ __attribute__((aligned(16))) u32x4_t lds[C::IN_U4 + C::W_U4];
@@ -384,7 +385,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_tiled_kernel(ConvK k, int tile
         const int q = seg * 64 + lane;
         const char* src = (const char*)g_dbsr_zero16;
         if (item < C::IN_ITEMS && q < C::NQ) {
-            const int iy = y0 - 1 + q / C::HWD, ix = x0 - 1 + q % C::HWD;
+            const int iy = y0 - D + q / C::HWD, ix = x0 - D + q % C::HWD;
             if ((unsigned)iy < (unsigned)k.in_h && (unsigned)ix < (unsigned)k.in_w)
                 src = (const char*)(xf + ((long long)iy * k.in_w + ix) * k.x_ld + gg * 8 + h * 4);
         }
@@ -438,7 +439,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_tiled_kernel(ConvK k, int tile
         }
 #pragma unroll
         for (int j = 0; j < WN / 16; ++j) {
-            const u32x4_t* p = lb_in + (j + ky) * C::HWD + kx;
+            const u32x4_t* p = lb_in + (j + ky * D) * C::HWD + kx * D;
             if constexpr (sizeof(T) == 2) {
                 b[j].v = __builtin_bit_cast(bf16x8_t, p[0]);
             } else {
@@ -573,9 +574,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_tiled_kernel(ConvK k, int tile
     }
 }
 
-template <typename T, int WM, int WN>
+template <typename T, int WM, int WN, int D>
 int launch_tiled(const ConvK& k, int n_frames, hipStream_t s) {
-    using C = TileCfg<T, WM, WN>;
+    using C = TileCfg<T, WM, WN, D>;
     const int tiles_x = (k.out_w + C::TW - 1) / C::TW, tiles_y = (k.out_h + C::TH - 1) / C::TH;
     const int nct = (k.cout + WM - 1) / WM;
     const long long nb = (long long)n_frames * tiles_x * tiles_y * nct;
@@ -583,7 +584,7 @@ int launch_tiled(const ConvK& k, int n_frames, hipStream_t s) {
         dbsr_set_error("conv2d: grid too large");
         return DBSR_E_ARG;
     }
-    hipLaunchKernelGGL((conv3x3_tiled_kernel<T, WM, WN>), dim3((unsigned)nb), dim3(256), 0, s, k, tiles_x, tiles_y,
+    hipLaunchKernelGGL((conv3x3_tiled_kernel<T, WM, WN, D>), dim3((unsigned)nb), dim3(256), 0, s, k, tiles_x, tiles_y,
                        nct, (int)nb);
     DBSR_LAUNCH_CHECK();
     return 0;
@@ -636,19 +637,58 @@ void pick_generic_tile(const ConvK& k, int& best_m, int& best_n) {
     }
 }
 
+// 3x3 'same' convolutions (pad == dilation) with dilation 1/2/4/8 (the PWC refiner's context
+// network, pwcnet.py:227-241, has 2/4/8; fp32 tiles with dilation 8 exceed the LDS)
 bool use_tiled(const dbsr_conv_desc* d) {
-    return !d->precise && cin_pad(d->cin) * (d->x.dtype == DBSR_BF16 ? 2 : 4) + 64 <= ZERO_PAGE_BYTES && d->kh == 3 && d->kw == 3 && d->stride == 1 && d->pad == 1 && d->dil == 1 && d->cin > 16 &&
-           d->out_h >= 8 && d->out_w >= 8 && d->out_mode == DBSR_OUT_NHWC && g_tiled_enabled;
+    const bool bf = d->x.dtype == DBSR_BF16;
+    const bool dil_ok = (d->dil == 1 || d->dil == 2 || d->dil == 4 || (d->dil == 8 && bf)) && d->pad == d->dil;
+    return !d->precise && cin_pad(d->cin) * (bf ? 2 : 4) + 64 <= ZERO_PAGE_BYTES && d->kh == 3 && d->kw == 3 &&
+           d->stride == 1 && dil_ok && d->cin > 16 && d->out_h >= 8 && d->out_w >= 8 &&
+           d->out_mode == DBSR_OUT_NHWC && g_tiled_enabled;
+}
+
+// Tile shape: 64 couts x 16x16 pixels by default; 32 couts for narrow convs (and 32x16 pixels on
+// large images); when the grid would leave CUs idle (< 2 blocks per CU: PWC coarse levels, the
+// 8-frame decoder convs) first 32 couts, then 16x4-pixel tiles.
+int tiled_blocks(const dbsr_conv_desc* d, int wm, int wn) {
+    const int th = 4 * wn / 16;
+    return d->n_frames * ((d->out_w + 15) / 16) * ((d->out_h + th - 1) / th) * ((d->cout + wm - 1) / wm);
+}
+void pick_tiled_tile(const dbsr_conv_desc* d, int& wm, int& wn) {
+    wm = d->cout <= 32 ? 32 : 64;
+    wn = (wm == 32 && d->out_h >= 32) ? 128 : 64;
+    if (tiled_blocks(d, wm, wn) >= 512) return;
+    if (wm == 64) {
+        wm = 32;
+        if (tiled_blocks(d, wm, wn) >= 512) return;
+    }
+    wn = 64;
+    if (tiled_blocks(d, wm, wn) >= 512) return;
+    wn = 16;
+}
+
+template <typename T, int D>
+int dispatch_tiled_d(const ConvK& k, const dbsr_conv_desc* d, hipStream_t s) {
+    int wm, wn;
+    pick_tiled_tile(d, wm, wn);
+    if (wm == 64) return launch_tiled<T, 64, 64, D>(k, d->n_frames, s);
+    if (wn == 128) return launch_tiled<T, 32, 128, D>(k, d->n_frames, s);
+    if (wn == 64) return launch_tiled<T, 32, 64, D>(k, d->n_frames, s);
+    return launch_tiled<T, 32, 16, D>(k, d->n_frames, s);
 }
 
 template <typename T>
 int dispatch_conv(const ConvK& k, const dbsr_conv_desc* d, hipStream_t s) {
     if (use_tiled(d)) {
-        if (k.cout <= 32) {
-            if (d->out_h >= 32) return launch_tiled<T, 32, 128>(k, d->n_frames, s);   // 32x16 tiles
-            return launch_tiled<T, 32, 64>(k, d->n_frames, s);                       // 16x16 tiles
+        switch (d->dil) {
+            case 1: return dispatch_tiled_d<T, 1>(k, d, s);
+            case 2: return dispatch_tiled_d<T, 2>(k, d, s);
+            case 4: return dispatch_tiled_d<T, 4>(k, d, s);
+            default:
+                if constexpr (sizeof(T) == 2) return dispatch_tiled_d<T, 8>(k, d, s);
+                dbsr_set_error("conv2d: no fp32 tile for dilation %d", d->dil);
+                return DBSR_E_ARG;
         }
-        return launch_tiled<T, 64, 64>(k, d->n_frames, s);
     }
     int best_m, best_n;
     pick_generic_tile(k, best_m, best_n);

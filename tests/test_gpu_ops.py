@@ -80,6 +80,15 @@ CONV_CASES = [
     (2, 565, 16, 16, 2, 3, 1, 1, 1),       # split-K (2-channel flow head)
     (104, 529, 1, 1, 32, 3, 1, 1, 1),      # split-K (PWC level 6)
     (7, 469, 4, 4, 64, 3, 1, 1, 1),        # split-K (PWC level 4)
+    (2, 128, 16, 16, 128, 3, 1, 2, 2),     # tiled kernel, dilation 2 (PWC refiner)
+    (2, 128, 19, 16, 128, 3, 1, 4, 4),     # tiled kernel, dilation 4, partial tile
+    (1, 64, 48, 48, 64, 3, 1, 1, 1),       # tiled kernel, small grid -> 16x4-pixel tiles
+]
+DILATED_BF16 = [
+    (2, 128, 16, 16, 128, 3, 1, 2, 2),
+    (2, 128, 16, 16, 128, 3, 1, 4, 4),
+    (2, 128, 16, 16, 96, 3, 1, 8, 8),
+    (3, 96, 20, 16, 64, 3, 1, 8, 8),
 ]
 
 
@@ -95,7 +104,7 @@ def test_conv2d_fp32(ops, case):
     np.testing.assert_allclose(out.numpy(), ref.numpy(), atol=2e-5, rtol=1e-4)
 
 
-@pytest.mark.parametrize('case', CONV_CASES[:4])
+@pytest.mark.parametrize('case', CONV_CASES[:4] + DILATED_BF16 + CONV_CASES[-1:])
 def test_conv2d_bf16(ops, case):
     N, Cin, H, W, Cout, k, s, p, d = case
     gen = torch.Generator().manual_seed(Cin * 1000 + Cout + 1)
