@@ -654,11 +654,15 @@ int tiled_blocks(const dbsr_conv_desc* d, int wm, int wn) {
     const int th = 4 * wn / 16;
     return d->n_frames * ((d->out_w + 15) / 16) * ((d->out_h + th - 1) / th) * ((d->cout + wm - 1) / wm);
 }
+#ifndef DBSR_TILE_WM32_MAX_COUT
+#define DBSR_TILE_WM32_MAX_COUT 64      // wider convs keep 64-cout tiles (halving re-reads the halo twice)
+#endif
 void pick_tiled_tile(const dbsr_conv_desc* d, int& wm, int& wn) {
     wm = d->cout <= 32 ? 32 : 64;
     wn = (wm == 32 && d->out_h >= 32) ? 128 : 64;
     if (tiled_blocks(d, wm, wn) >= 512) return;
     if (wm == 64) {
+        if (d->cout > DBSR_TILE_WM32_MAX_COUT && d->out_w > 8) return;   // 8x8 PWC level 3: parallelism wins
         wm = 32;
         if (tiled_blocks(d, wm, wn) >= 512) return;
     }

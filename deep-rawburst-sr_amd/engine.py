@@ -107,6 +107,7 @@ class Plan:
     capture alike.
     """
     FORK, JOIN = '__fork__', '__join__'
+    MULTI_STREAM = True      # False: every lane runs on the caller's stream (debug / A-B timing)
 
     def __init__(self):
         self.ops = []        # (callable | FORK | JOIN, args, name, lane)
@@ -126,6 +127,8 @@ class Plan:
     def fork(self, lane, device, priority=0):
         """Following ops go to side stream `lane`, ordered after everything issued so far on lane 0."""
         assert self.lane == 0 and lane != 0
+        if not Plan.MULTI_STREAM:
+            return
         if lane not in self.streams:
             self.streams[lane] = torch.cuda.Stream(device=device, priority=priority)
         self.lanes.add(lane)
@@ -134,11 +137,13 @@ class Plan:
 
     def switch(self, lane):
         """Following ops go to `lane` (an already forked side lane, or 0), with no ordering edge."""
-        assert lane == 0 or lane in self.streams
-        self.lane = lane
+        assert lane == 0 or lane in self.streams or not Plan.MULTI_STREAM
+        self.lane = lane if Plan.MULTI_STREAM else 0
 
     def join(self, lane):
         """Lane 0 waits for all work issued so far on side lane `lane`; following ops go to lane 0."""
+        if not Plan.MULTI_STREAM:
+            return
         assert lane != 0 and lane in self.streams
         self.ops.append((Plan.JOIN, (torch.cuda.Event(),), f'sync.join{lane}', lane))
         self.lane = 0
@@ -272,6 +277,7 @@ class PWCPlanner:
             plan.conv(f'pwc.ext{k + 1}.2', self.ext[k][1], nF, ta, 0, (oh, ow), tb, 0, L.ACT_LRELU)
             plan.conv(f'pwc.ext{k + 1}.4', self.ext[k][2], nF, tb, 0, (oh, ow), lv, 0, L.ACT_LRELU)
             levels[k + 1] = lv
+            plan.keep.extend([ta, tb])      # every buffer a launch touches lives as long as the plan
             x, hw = lv, (oh, ow)
         plan.keep.append(levels)
         # ---- decoders, coarse to fine (pwcnet.py:225-229, Decoder.forward :153-184) ----
