@@ -25,14 +25,15 @@ $(LIB): $(OBJS)
 
 # Experiment build: same sources with extra -D flags, loaded via DBSR_HIP_LIB for A/B profiling.
 EXP_FLAGS ?=
-EXP_LIB   := $(PKG)/libdbsr_hip_exp.so
+EXP_NAME  ?= exp
+EXP_LIB   := $(PKG)/libdbsr_hip_$(EXP_NAME).so
 exp:
-	@mkdir -p $(OBJDIR)/exp
+	@mkdir -p $(OBJDIR)/$(EXP_NAME)
 	for f in $(HIPSRCS) $(CPPSRCS); do \
-	  $(HIPCC) $(FLAGS) $(EXP_FLAGS) -c $$f -o $(OBJDIR)/exp/$$(basename $$f).o || exit 1; done
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(EXP_LIB) $(OBJDIR)/exp/*.o
+	  $(HIPCC) $(FLAGS) $(EXP_FLAGS) -c $$f -o $(OBJDIR)/$(EXP_NAME)/$$(basename $$f).o || exit 1; done
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(EXP_LIB) $(OBJDIR)/$(EXP_NAME)/*.o
 
 clean:
-	rm -rf $(OBJDIR) $(LIB) $(EXP_LIB)
+	rm -rf $(OBJDIR) $(LIB) $(PKG)/libdbsr_hip_*.so
 
 .PHONY: all clean exp

@@ -29,7 +29,7 @@ inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
 // conv with cin > 16 is a whole number of 32-channel MFMA chunks per tap
 inline int cin_pad(int cin) { return cin <= 16 ? round_up(cin, 8) : round_up(cin, 32); }
 
-int g_tiled_enabled = 1;   // dbsr_set_conv_algo: 0 generic only, 1 LDS-tiled where applicable
+int g_tiled_enabled = 1;   // dbsr_set_conv_algo: 0 generic only, 1 LDS-tiled where applicable, 2 + pipelined
 
 struct ConvK {
     const void* x; long long x_is; int x_ld; dbsr_frame_map xm; int in_h, in_w;
@@ -43,6 +43,7 @@ struct ConvK {
     int ksplit;        // K slices (generic kernel); > 1: fp32 partials to ws, summed by conv_splitk_finalize
     float* ws;         // [ksplit][npix][cw] fp32
     int cw;            // round_up(cout, 4)
+    const void* w_pipe;  // chunk-major weight copy (3x3, cin > 16): [cout/16][chunk][tap][4 k-groups][16 co][8]
 };
 
 template <typename T> struct Frag;
@@ -261,6 +262,27 @@ __global__ __launch_bounds__(256) void conv_splitk_finalize(ConvK k) {
     f32x4_t a = {0.f, 0.f, 0.f, 0.f};
     for (int z = 0; z < k.ksplit; ++z) a += *(const f32x4_t*)(k.ws + ((long long)z * k.npix + p) * k.cw + co);
     epilogue_px<T>(k, p, co, a, load_bias4(k, co));
+}
+
+// row layout [cout_pad][Kp] -> chunk-major pieces [cout_pad/16][chunk][tap][g][16 co][8] (3x3, cin > 16);
+// within each tile of P = (cout <= 32 ? 32 : 64) couts, row col of 16-cout block blk holds physical cout
+// pipe_cout_perm(blk, col) (the pipelined kernel's 8-consecutive-couts-per-lane epilogue order)
+__host__ __device__ __forceinline__ int pipe_cout_perm(int i, int m) {
+    return 32 * (i >> 1) + 8 * (m >> 2) + 4 * (i & 1) + (m & 3);
+}
+__global__ void pack_weights_pipe_kernel(const bf16_t* __restrict__ rows, int CG, int Kp, int P, long long total,
+                                         bf16_t* __restrict__ out) {
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= total) return;
+    const int e = (int)(idx & 7), col = (int)((idx >> 3) & 15), g = (int)((idx >> 7) & 3);
+    long long piece = idx >> 9;
+    const int tap = (int)(piece % 9); piece /= 9;
+    const int nch = CG / 4;
+    const int c = (int)(piece % nch);
+    const long long cb16 = piece / nch;
+    const int bpt = P / 16;                                   // 16-cout blocks per tile
+    const long long co = (cb16 / bpt) * P + pipe_cout_perm((int)(cb16 % bpt), col);
+    out[idx] = rows[co * Kp + (tap * CG + c * 4 + g) * 8 + e];
 }
 
 __global__ void pack_weights_kernel(const float* __restrict__ w, const float* __restrict__ bias, int cout, int cin,
@@ -590,6 +612,369 @@ int launch_tiled(const ConvK& k, int n_frames, hipStream_t s) {
     return 0;
 }
 
+// ------------------------------------------------------------------------------------------------
+// Pipelined LDS-tiled 3x3 conv (bf16, stride 1, pad 1, dilation 1) for the large trunk convs: the
+// encoder and weight-predictor ResNets at 48x48 and the decoder's 384x384 ResBlocks.
+//
+// One 512-thread block per CU, persistent over output tiles (WM couts x TH rows x TW pixels of one
+// frame).  The work of a block is a sequence of stages, one per (tile, 32-channel chunk); a stage
+// image (halo + the chunk's weights for all 9 taps) is staged by LDS-DMA into one of two LDS
+// buffers.  Stage s+1's DMA is issued while stage s's 9 taps of MFMAs run -- one or two 1-KiB pieces
+// per tap, never in a burst: s_memtime stamps of a burst-issue version showed every wave parked ~2k
+// cycles per stage in the vector-memory issue queue (72 pieces per CU at ~28 cycles each through the
+// texture-address path) before its first MFMA.  The tile epilogue works from registers: its residual
+// loads and its (deferred, one stage later) output stores are spread over the taps the same way, so
+// the only exposed wait per stage is one barrier.
+// 8 waves = the TH rows of the tile: wave w owns row w (TW/16 groups of 16 pixels) x all WM couts.
+// Per stage: weights 9*WM*64 B + halo (TH+2)(TW+2)*64 B for 2*WM*TW*TH*288 FLOP, i.e. 203 FLOP/B at
+// (WM, TW, TH) = (64, 48, 8) against 153 for the 64 x 16x16 tile of the two-barrier kernel.
+//
+// Cout order inside a WM tile (weights and bias permuted by the packer, pipe_cout_perm): MFMA row m of
+// 16-cout block i is physical cout 32(i>>1) + 8(m>>2) + 4(i&1) + (m&3), so the accumulators of blocks
+// 2h and 2h+1 give lane (g, col) 8 consecutive couts of its pixel: 16-B residual loads and stores.
+// ------------------------------------------------------------------------------------------------
+template <int WM, int TW, int TH>
+struct PipeCfg {
+    static constexpr int NWAVES = 8;                          // two waves per SIMD (256-VGPR budget)
+    static constexpr int RPW = TH / NWAVES;                   // tile rows per wave
+    static constexpr int HWD = TW + 2, HHT = TH + 2;
+    static constexpr int NQ = HWD * HHT;                      // halo pixels
+    static constexpr int IN_ITEMS = (NQ + 15) / 16;           // halo pieces: 16 pixels x 64 B (4 k-groups)
+    static constexpr int W_ITEMS = 9 * (WM / 16);             // weight pieces (tap, 16-cout block)
+    static constexpr int ITEMS = IN_ITEMS + W_ITEMS;
+    static constexpr int PER = (ITEMS + NWAVES - 1) / NWAVES; // DMA pieces per wave per stage (uniform)
+    static constexpr int STAGE_U4 = ITEMS * 64;               // 16-B slots per stage buffer
+    static constexpr int GPR = TW / 16;                       // 16-pixel groups per row
+    static constexpr int GW = GPR * RPW;                      // pixel groups per wave
+    static constexpr int NH = WM / 32;                        // 8-cout lane runs per pixel
+    static constexpr int NOUT = NH * GW;                      // 16-B outputs per lane per tile
+    static constexpr int BIAS_U4 = 512 / 4;                   // bias region: cout <= 512 floats
+    static constexpr int LDS_U4 = 2 * STAGE_U4 + BIAS_U4;
+    static_assert(TH % NWAVES == 0, "whole tile rows per wave");
+    static_assert(TW % 16 == 0 && (WM == 32 || WM == 64), "tile shape");
+    static_assert(LDS_U4 * 16 <= 160 * 1024, "two stage buffers + bias must fit the LDS");
+};
+
+// Pixel-major halo image: halo pixel p holds its chunk's 4 k-groups (64 B) in slots 4p..4p+3, k-group g
+// at slot 4p + phys(p, g) with phys(p, g) = 2(g&1) + ((g>>1) ^ ((p>>2)&1)).  A DMA piece is then 16
+// pixels x 64 B, i.e. 16 cache lines per wave-instruction instead of the 64 of a planar [k-group][pixel]
+// piece, and the swizzle keeps every B-fragment ds_read_b128 conflict-free for any tap shift: within
+// each of its four 16-lane groups, the 4 lanes with equal p mod 4 read 4 distinct phys values.
+__device__ __forceinline__ int halo_phys(int p, int g) { return 2 * (g & 1) + ((g >> 1) ^ ((p >> 2) & 1)); }
+
+#ifdef DBSR_PIPE_STAMPS
+// diagnostic build only: per-block s_memtime stamps of wave 0 (tools/pipe_stamps.py)
+constexpr int STAMP_BLOCKS = 256, STAMP_N = 128;
+__device__ unsigned long long g_pipe_stamps[STAMP_BLOCKS][STAMP_N];
+#define PIPE_STAMP(idx)                                                                          \
+    do {                                                                                         \
+        if (threadIdx.x == 0 && blockIdx.x < STAMP_BLOCKS && (idx) < STAMP_N)                    \
+            g_pipe_stamps[blockIdx.x][(idx)] = __builtin_amdgcn_s_memtime();                     \
+    } while (0)
+#else
+#define PIPE_STAMP(idx) do {} while (0)
+#endif
+
+template <int WM, int TW, int TH, int EPI>
+__global__ __launch_bounds__(512, 1) void conv3x3_pipe_kernel(ConvK k, int tiles_x, int tiles_y, int nct,
+                                                              int ntiles) {
+    using C = PipeCfg<WM, TW, TH>;
+    typedef bf16_t T;
+    __shared__ __attribute__((aligned(16))) u32x4_t lds[C::LDS_U4];
+    float* lbias = (float*)(lds + 2 * C::STAGE_U4);      // [nct * WM] fp32
+
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int g = lane >> 4, col = lane & 15;
+    const int nchunks = k.CG / 4;
+    // epilogue variants (compile-time where the forward's convs need them): 1 act(ReLU), 2 conv + residual
+    // then ReLU (ResBlock conv2), 3 plain; 0 reads act / residual / post_act at run time
+    const bool has_res = EPI == 2 || (EPI == 0 && k.r != nullptr);
+    auto act1 = [&](float v) {
+        if constexpr (EPI == 1) return fmaxf(v, 0.f);
+        else if constexpr (EPI == 0) return apply_act(v, k.act);
+        else return v;
+    };
+    auto act2 = [&](float v) {
+        if constexpr (EPI == 2) return fmaxf(v, 0.f);
+        else if constexpr (EPI == 0) return apply_act(v, k.post_act);
+        else return v;
+    };
+
+    // bias into LDS once; ordered before its first read by the loop's first barrier
+    for (int c = threadIdx.x; c < nct * WM; c += 512) lbias[c] = (k.bias && c < k.cout) ? k.bias[c] : 0.f;
+
+    // persistent tile walk, XCD-grouped: the blocks sharing an XCD (equal blockIdx % 8) take a
+    // contiguous range of tile ids per round, so a spatial tile's cout tiles and neighbouring halos
+    // meet in one L2 (grid is a multiple of 8)
+    const int grid = gridDim.x, b = blockIdx.x;
+    const int pb = (b & 7) * (grid >> 3) + (b >> 3);
+    const int my_tiles = pb < ntiles ? (ntiles - pb + grid - 1) / grid : 0;
+    if (my_tiles == 0) return;
+
+    // tile descriptors hold wave-uniform values only (scalar registers); the lane's own pixel/cout offset
+    // within a tile is the same for every tile
+    struct Tile { const T* xf; long long y_off, r_off; int y0, x0, cb; };
+    auto decode = [&](int i) {
+        int L = i * grid + pb;
+        const int ct = L % nct; L /= nct;
+        const int tx = L % tiles_x; L /= tiles_x;
+        const int ty = L % tiles_y;
+        const int f = L / tiles_y;
+        Tile t;
+        t.y0 = ty * TH; t.x0 = tx * TW; t.cb = ct * WM;
+        t.xf = (const T*)k.x + map_frame(k.xm, f) * k.x_is;
+        const long long pix = (long long)t.y0 * k.out_w + t.x0;
+        t.y_off = map_frame(k.ym, f) * k.y_is + k.y_c0 + t.cb + pix * k.y_ld;
+        t.r_off = has_res ? map_frame(k.rm, f) * k.r_is + k.r_c0 + t.cb + pix * k.r_ld : 0;
+        return t;
+    };
+    const long long y_lane = (long long)(wave * C::RPW * k.out_w + col) * k.y_ld + g * 8;
+    const long long r_lane = has_res ? (long long)(wave * C::RPW * k.out_w + col) * k.r_ld + g * 8 : 0;
+    // pixel-group jj of a wave = row jj / GPR of its RPW rows, 16-pixel column group jj % GPR
+    auto grp_off = [&](int jj) { return (long long)(jj / C::GPR) * k.out_w + (jj % C::GPR) * 16; };
+
+    // one 1-KiB DMA piece of stage (tile t, chunk c): piece `it` of this wave is item wave + 8*it of the
+    // stage image (clamped: surplus slots re-issue the last piece, an identical write, so every wave
+    // issues exactly PER pieces); addresses are computed at issue time, between MFMAs
+    auto dma = [&](int it, const Tile& t, int c, int buf) {
+        const int item = min(wave + C::NWAVES * it, C::ITEMS - 1);
+        const char* src;
+        if (item < C::IN_ITEMS) {
+            // lane -> (halo pixel, physical k-group slot) -> logical k-group (inverse of halo_phys)
+            const int p = item * 16 + (lane >> 2), ph = lane & 3;
+            const int gg = 2 * ((ph & 1) ^ ((p >> 2) & 1)) + (ph >> 1);
+            const int r = p / C::HWD, cc = p - (p / C::HWD) * C::HWD;
+            const int iy = t.y0 - 1 + r, ix = t.x0 - 1 + cc;
+            src = (p < C::NQ && (unsigned)iy < (unsigned)k.in_h && (unsigned)ix < (unsigned)k.in_w)
+                      ? (const char*)(t.xf + ((long long)iy * k.in_w + ix) * k.x_ld + c * 32 + gg * 8)
+                      : (const char*)g_dbsr_zero16;
+        } else {
+            // chunk-major weight copy: one contiguous 1-KiB piece per (16-cout block, chunk, tap)
+            const int wi = item - C::IN_ITEMS;
+            const int tap = wi / (WM / 16), blk = wi % (WM / 16);
+            const long long piece = ((long long)((t.cb >> 4) + blk) * nchunks + c) * 9 + tap;
+            src = (const char*)((const T*)k.w_pipe + piece * 512 + lane * 8);
+        }
+#ifndef DBSR_PIPE_NO_DMA
+        glds16(src, lds + buf * C::STAGE_U4 + item * 64);
+#else
+        asm volatile("" ::"v"(src), "v"(buf));
+#endif
+    };
+
+    f32x4_t acc[WM / 16][C::GW];
+#pragma unroll
+    for (int i = 0; i < WM / 16; ++i)
+#pragma unroll
+        for (int j = 0; j < C::GW; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    u32x4_t resv[C::NOUT];              // residual of the tile being computed (loaded in its last stage)
+    u32x4_t pend[C::NOUT];              // packed outputs of the last finished tile (stored next stage)
+
+    // lane-dependent LDS bases within a stage buffer; tap/fragment offsets are immediates.  Halo pixel
+    // P0 + imm of k-group g sits at slot 4(P0 + imm) + halo_phys(P0 + imm, g), and halo_phys depends on
+    // imm only through imm & 7, so 8 per-lane bases cover every (tap, group) offset.
+    const int P0 = wave * C::RPW * C::HWD + col;
+    int in_base[8];
+#pragma unroll
+    for (int rho = 0; rho < 8; ++rho) in_base[rho] = 4 * P0 + halo_phys(P0 + rho, g);
+    const int w_base = C::IN_ITEMS * 64 + g * 16 + col;
+
+    // Epilogue of a finished tile, right after the barrier that follows its last stage (its residual,
+    // loaded during that stage, has landed; no DMA is in flight yet): output piece q = (8-cout run h,
+    // pixel group j) -- lane (g, col) holds couts cb + 32h + 8g .. +7 of its pixel in acc[2h][j] and
+    // acc[2h+1][j] -- gets bias + act (+ residual + post-act) and is packed to bf16 for a 16-B store
+    // during the next stage's taps; the accumulators restart from zero.
+    auto epilogue = [&](const Tile& t) {
+#pragma unroll
+        for (int q = 0; q < C::NOUT; ++q) {
+            const int h = q / C::GW, j = q % C::GW;
+            const float4 b0 = *(const float4*)(lbias + t.cb + 32 * h + 8 * g);
+            const float4 b1 = *(const float4*)(lbias + t.cb + 32 * h + 8 * g + 4);
+            const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+            float v[8];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                v[r] = act1(acc[2 * h][j][r] + bv[r]);
+                v[4 + r] = act1(acc[2 * h + 1][j][r] + bv[4 + r]);
+            }
+            if (has_res) {
+                const u32x4_t rq = resv[q];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    v[2 * e] = act2(v[2 * e] + __uint_as_float(rq[e] << 16));
+                    v[2 * e + 1] = act2(v[2 * e + 1] + __uint_as_float(rq[e] & 0xffff0000u));
+                }
+            }
+            u32x4_t o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = pack_bf16x2(v[2 * e], v[2 * e + 1]);
+            pend[q] = o;
+            acc[2 * h][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+            acc[2 * h + 1][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        }
+    };
+    auto store_piece = [&](int q, const Tile& t) {   // runs of couts >= cout (partial cout tile) skipped
+        const int h = q / C::GW, j = q % C::GW;
+        if (t.cb + 32 * h + 8 * g < k.cout)
+            *(u32x4_t*)((T*)k.y + t.y_off + y_lane + grp_off(j) * k.y_ld + 32 * h) = pend[q];
+    };
+
+    int s = 0;                          // global stage index (LDS buffer = s & 1)
+    Tile cur = decode(0), prev = cur;
+    PIPE_STAMP(0);
+#pragma unroll
+    for (int it = 0; it < C::PER; ++it) dma(it, cur, 0, 0);
+
+    // Per stage: barrier, [epilogue of the previous tile], then the 9 taps with this stage's
+    // vector-memory work spread between their MFMAs: the previous tile's output stores, this tile's
+    // residual loads (last stage) and the next stage's DMA pieces (taps 0-5).
+    for (int ti = 0; ti < my_tiles; ++ti) {
+        for (int c = 0; c < nchunks; ++c, ++s) {
+            PIPE_STAMP(1 + 3 * s);
+            __syncthreads();            // stage s landed (vmcnt(0) + barrier); stage s-1 fully consumed
+            PIPE_STAMP(2 + 3 * s);
+            const bool fin = c == 0 && ti > 0;
+            if (fin) epilogue(prev);
+            const bool last = c == nchunks - 1;
+            const bool more = !(last && ti + 1 == my_tiles);
+            Tile nxt = cur;
+            const int nc = last ? 0 : c + 1;
+            if (last && more) nxt = decode(ti + 1);
+            const u32x4_t* lb_st = lds + (s & 1) * C::STAGE_U4;
+            const u32x4_t* lb_w = lb_st + w_base;
+            const int nbuf = (s + 1) & 1;
+            auto vmem = [&](int tap) {
+#pragma unroll
+                for (int q = 0; q < C::NOUT; ++q) {
+                    if ((q * 9) / C::NOUT != tap) continue;       // output pieces spread over the 9 taps
+                    if (fin) store_piece(q, prev);
+                    if (has_res && last) {
+                        const int h = q / C::GW, j = q % C::GW;
+                        const bool ok = cur.cb + 32 * h + 8 * g < k.cout;
+                        resv[q] = *(const u32x4_t*)((const T*)k.r + cur.r_off + r_lane + grp_off(j) * k.r_ld +
+                                                    (ok ? 32 * h : 0));
+                    }
+                }
+                if (more) {
+#pragma unroll
+                    for (int it = 0; it < C::PER; ++it)
+                        if ((it * 6) / C::PER == tap) dma(it, nxt, nc, nbuf);
+                }
+            };
+            auto read_frags = [&](int tap, Frag<T> (&a)[WM / 16], Frag<T> (&bq)[C::GW]) {
+                const int ky = tap / 3, kx = tap % 3;
+#pragma unroll
+                for (int i = 0; i < WM / 16; ++i) a[i].v = __builtin_bit_cast(bf16x8_t, lb_w[(tap * (WM / 16) + i) * 64]);
+#pragma unroll
+                for (int j = 0; j < C::GW; ++j) {
+                    const int imm = (j / C::GPR + ky) * C::HWD + (j % C::GPR) * 16 + kx;
+                    bq[j].v = __builtin_bit_cast(bf16x8_t, lb_st[in_base[imm & 7] + 4 * imm]);
+                }
+            };
+            auto mfmas = [&](const Frag<T> (&a)[WM / 16], const Frag<T> (&bq)[C::GW]) {
+#ifndef DBSR_PIPE_NO_MFMA
+#pragma unroll
+                for (int i = 0; i < WM / 16; ++i)
+#pragma unroll
+                    for (int j = 0; j < C::GW; ++j) acc[i][j] = mma(a[i], bq[j], acc[i][j]);
+#else
+#pragma unroll
+                for (int i = 0; i < WM / 16; ++i) asm volatile("" ::"v"(a[i].v));
+#pragma unroll
+                for (int j = 0; j < C::GW; ++j) asm volatile("" ::"v"(bq[j].v));
+#endif
+            };
+            Frag<T> a0[WM / 16], b0[C::GW], a1[WM / 16], b1[C::GW];
+            read_frags(0, a0, b0);
+#pragma unroll
+            for (int tap = 0; tap < 9; tap += 2) {
+                vmem(tap);
+                if (tap + 1 < 9) read_frags(tap + 1, a1, b1);
+                mfmas(a0, b0);
+                if (tap + 1 < 9) {
+                    vmem(tap + 1);
+                    if (tap + 2 < 9) read_frags(tap + 2, a0, b0);
+                    mfmas(a1, b1);
+                }
+            }
+            PIPE_STAMP(3 + 3 * s);
+            if (last) {
+                prev = cur;
+                cur = nxt;
+            }
+        }
+    }
+    __syncthreads();                    // the last tile's residual landed (vmcnt(0))
+    epilogue(prev);
+#pragma unroll
+    for (int q = 0; q < C::NOUT; ++q) store_piece(q, prev);
+    PIPE_STAMP(STAMP_N - 1 > 3 * s + 1 ? 3 * s + 1 : STAMP_N - 1);
+}
+
+int g_num_cus = 0;
+int num_cus() {
+    if (g_num_cus == 0) {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+            g_num_cus = n;
+        else
+            g_num_cus = 256;
+    }
+    return g_num_cus;
+}
+
+template <int WM, int TW, int TH>
+int launch_pipe(const ConvK& k, int n_frames, hipStream_t s) {
+    const int tiles_x = (k.out_w + TW - 1) / TW, tiles_y = (k.out_h + TH - 1) / TH;
+    const int nct = (k.cout + WM - 1) / WM;
+    const long long nt = (long long)n_frames * tiles_x * tiles_y * nct;
+    if (nt >= (1LL << 31)) {
+        dbsr_set_error("conv2d: grid too large");
+        return DBSR_E_ARG;
+    }
+    int grid = (int)std::min<long long>(nt, num_cus());
+    grid = (grid + 7) / 8 * 8;
+    // compile-time epilogues for the forward's three conv flavours, run-time otherwise
+    int epi = 0;
+    if (!k.r && k.act == DBSR_ACT_RELU) epi = 1;
+    else if (k.r && k.act == DBSR_ACT_NONE && k.post_act == DBSR_ACT_RELU) epi = 2;
+    else if (!k.r && k.act == DBSR_ACT_NONE) epi = 3;
+#define DBSR_PIPE_LAUNCH(E)                                                                                    \
+    hipLaunchKernelGGL((conv3x3_pipe_kernel<WM, TW, TH, E>), dim3(grid), dim3(512), 0, s, k, tiles_x, tiles_y, \
+                       nct, (int)nt)
+    switch (epi) {
+        case 1: DBSR_PIPE_LAUNCH(1); break;
+        case 2: DBSR_PIPE_LAUNCH(2); break;
+        case 3: DBSR_PIPE_LAUNCH(3); break;
+        default: DBSR_PIPE_LAUNCH(0); break;
+    }
+#undef DBSR_PIPE_LAUNCH
+    DBSR_LAUNCH_CHECK();
+    return 0;
+}
+
+// which pipelined tile serves `d` (0: none): bf16 3x3/s1/p1/d1 with Cin % 32 == 0 after padding, an
+// aligned NHWC bf16 output (staged epilogue), and enough tiles to fill the chip
+int g_pipe_enabled = 1;
+int pick_pipe(const dbsr_conv_desc* d) {
+    if (!g_pipe_enabled || d->x.dtype != DBSR_BF16 || d->precise || d->kh != 3 || d->kw != 3 || d->stride != 1 ||
+        d->pad != 1 || d->dil != 1 || d->cin <= 16 || d->out_mode != DBSR_OUT_NHWC || d->y.dtype != DBSR_BF16)
+        return 0;
+    if (d->y.ld % 8 || d->y.c0 % 8 || d->cout % 8 || (d->res.ptr && (d->res.ld % 8 || d->res.c0 % 8))) return 0;
+    if (cin_pad(d->cin) * 2 + 64 > ZERO_PAGE_BYTES || d->cout > 512) return 0;
+    int cfg = 0, tw = 0, wm = 0;
+    if (d->cout > 32 && d->out_w % 48 == 0) { cfg = 1; tw = 48; wm = 64; }
+    else if (d->cout <= 32 && d->out_w % 64 == 0) { cfg = 2; tw = 64; wm = 32; }
+    if (!cfg || d->out_h % 8) return 0;
+    const long long nt = (long long)d->n_frames * (d->out_w / tw) * (d->out_h / 8) * ((d->cout + wm - 1) / wm);
+    return (nt >= 256 || g_pipe_enabled == 2) ? cfg : 0;
+}
+
+int dispatch_pipe(int cfg, const ConvK& k, const dbsr_conv_desc* d, hipStream_t s) {
+    if (cfg == 1) return launch_pipe<64, 48, 8>(k, d->n_frames, s);
+    return launch_pipe<32, 64, 8>(k, d->n_frames, s);
+}
+
 template <typename T, int MT, int NT, typename XT = T>
 int launch_conv(const ConvK& k, hipStream_t s) {
     dim3 grid((k.npix + 4 * NT * 16 - 1) / (4 * NT * 16), (k.cout + MT * 16 - 1) / (MT * 16), k.ksplit);
@@ -683,6 +1068,10 @@ int dispatch_tiled_d(const ConvK& k, const dbsr_conv_desc* d, hipStream_t s) {
 
 template <typename T>
 int dispatch_conv(const ConvK& k, const dbsr_conv_desc* d, hipStream_t s) {
+    if constexpr (sizeof(T) == 2) {
+        const int cfg = pick_pipe(d);
+        if (cfg) return dispatch_pipe(cfg, k, d, s);
+    }
     if (use_tiled(d)) {
         switch (d->dil) {
             case 1: return dispatch_tiled_d<T, 1>(k, d, s);
@@ -727,6 +1116,7 @@ ConvK make_convk(const dbsr_conv_desc* d) {
     k.ksplit = 1;
     k.ws = (float*)d->workspace;
     k.cw = round_up(d->cout, 4);
+    k.w_pipe = (const char*)d->w + (size_t)round_up(d->cout, 64) * k.Kp * esz;
     return k;
 }
 
@@ -734,11 +1124,12 @@ ConvK make_convk(const dbsr_conv_desc* d) {
 
 extern "C" int dbsr_conv_kernel_for(const dbsr_conv_desc* d) {
     if (!d) return -1;
+    if (pick_pipe(d)) return 2;
     return use_tiled(d) ? 1 : 0;
 }
 
 extern "C" size_t dbsr_conv_workspace_bytes(const dbsr_conv_desc* d) {
-    if (!d || use_tiled(d) || d->precise) return 0;
+    if (!d || pick_pipe(d) || use_tiled(d) || d->precise) return 0;
     const ConvK k = make_convk(d);
     int m, n;
     pick_generic_tile(k, m, n);
@@ -746,14 +1137,20 @@ extern "C" size_t dbsr_conv_workspace_bytes(const dbsr_conv_desc* d) {
 }
 
 extern "C" int dbsr_set_conv_algo(int algo) {
-    DBSR_CHECK_ARG(algo >= 0 && algo <= 1, "set_conv_algo: 0 generic, 1 tiled");
-    g_tiled_enabled = algo;
+    DBSR_CHECK_ARG(algo >= 0 && algo <= 3, "set_conv_algo: 0 generic, 1 two-barrier tiled, 2 pipelined + tiled, "
+                   "3 pipelined wherever the shape allows");
+    g_tiled_enabled = algo >= 1;
+    g_pipe_enabled = algo >= 2 ? algo - 1 : 0;
     return 0;
 }
 
+// packed weights carry the chunk-major copy for the pipelined kernel when it can apply
+inline bool has_pipe_copy(int cin, int kh, int kw) { return kh == 3 && kw == 3 && cin > 16; }
+
 extern "C" size_t dbsr_conv_packed_elems(int cout, int cin, int kh, int kw) {
     const int KGp = round_up(kh * kw * (cin_pad(cin) / 8), 4);
-    return (size_t)round_up(cout, 64) * KGp * 8;
+    const size_t rows = (size_t)round_up(cout, 64) * KGp * 8;
+    return has_pipe_copy(cin, kh, kw) ? 2 * rows : rows;
 }
 
 extern "C" int dbsr_conv_pack_weights(const float* w_f32, const float* bias_f32, int cout, int cin, int kh, int kw,
@@ -771,6 +1168,12 @@ extern "C" int dbsr_conv_pack_weights(const float* w_f32, const float* bias_f32,
                        w_f32, bias_f32, cout, cin, kh, kw, CG, KG, Kp, cout_pad, shuffle, dtype == DBSR_BF16 ? 1 : 0,
                        w_packed, bias_out);
     DBSR_LAUNCH_CHECK();
+    if (has_pipe_copy(cin, kh, kw) && dtype == DBSR_BF16) {
+        hipLaunchKernelGGL(pack_weights_pipe_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                           (hipStream_t)stream, (const bf16_t*)w_packed, CG, Kp, cout <= 32 ? 32 : 64, total,
+                           (bf16_t*)w_packed + total);
+        DBSR_LAUNCH_CHECK();
+    }
     return 0;
 }
 
@@ -812,3 +1215,14 @@ extern "C" int dbsr_conv2d(const dbsr_conv_desc* d, void* stream) {
     }
     return d->x.dtype == DBSR_BF16 ? dispatch_conv<bf16_t>(k, d, s) : dispatch_conv<float>(k, d, s);
 }
+
+#ifdef DBSR_PIPE_STAMPS
+extern "C" int dbsr_debug_pipe_stamps(unsigned long long* host, int n) {
+    const size_t bytes = std::min<size_t>((size_t)n, (size_t)STAMP_BLOCKS * STAMP_N) * sizeof(unsigned long long);
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pipe_stamps), bytes, 0, hipMemcpyDeviceToHost);
+}
+extern "C" int dbsr_debug_pipe_stamps_clear() {
+    static unsigned long long zeros[STAMP_BLOCKS * STAMP_N];
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_pipe_stamps), zeros, sizeof(zeros), 0, hipMemcpyHostToDevice);
+}
+#endif

@@ -173,7 +173,8 @@ class Plan:
         self.convs.append((d, self.lane))
         flop = 2.0 * n_frames * oh * ow * pc.cout * d.cin * pc.kh * pc.kw
         self.add(name, L.lib().dbsr_conv2d, ctypes.byref(d), work=('flop', flop))
-        self.kernel[len(self.ops) - 1] = 'conv3x3_tiled' if L.lib().dbsr_conv_kernel_for(d) == 1 else 'conv2d_generic'
+        self.kernel[len(self.ops) - 1] = {2: 'conv3x3_pipe', 1: 'conv3x3_tiled'}.get(L.lib().dbsr_conv_kernel_for(d),
+                                                                                      'conv2d_generic')
         return d
 
     def finalize_workspace(self, device):

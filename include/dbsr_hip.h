@@ -85,18 +85,25 @@ typedef struct dbsr_conv_desc {
 /* Packed weight layout: [cout_pad][kgp*8] with k-group kg = (ky*kw+kx)*(cinp/8) + c/8, where
  * cinp = cin <= 16 ? round_up(cin, 8) : round_up(cin, 32), kgp = round_up(kh*kw*cinp/8, 4),
  * cout_pad = round_up(cout, 64).  The conv reads input channels [c0, c0+cinp) of every pixel, so the
- * caller's slice must extend that far and channels [cin, cinp) must hold finite values (zeros). */
+ * caller's slice must extend that far and channels [cin, cinp) must hold finite values (zeros).
+ * For 3x3 convs with cin > 16 the row layout is followed (bf16 packing) by a chunk-major copy for
+ * the pipelined kernel: 1-KiB pieces [cout_pad/16][cinp/32][tap][4 k-groups][16 co][8], so
+ * dbsr_conv_packed_elems returns twice the row layout's size for them. */
 size_t dbsr_conv_packed_elems(int cout, int cin, int kh, int kw);
 /* w_f32: torch layout [cout][cin][kh][kw] fp32 (device).  bias_f32 may be NULL.  With shuffle > 1
  * the output channels are permuted for the DBSR_OUT_SHUFFLE epilogue (and bias_out likewise). */
 int dbsr_conv_pack_weights(const float* w_f32, const float* bias_f32, int cout, int cin, int kh, int kw,
                            int dtype, int shuffle, void* w_packed, float* bias_out, void* stream);
 int dbsr_conv2d(const dbsr_conv_desc* d, void* stream);
-/* Kernel selection for dbsr_conv2d (process-wide; for A/B testing): 1 (default) = LDS-tiled 3x3
- * kernel where it applies (3x3, stride 1, pad 1, dilation 1, cin > 16, out >= 8x8, NHWC out),
- * 0 = generic implicit-GEMM kernel only. */
+/* Kernel selection for dbsr_conv2d (process-wide; for A/B testing): 2 (default) = pipelined
+ * persistent 3x3 kernel for the large bf16 trunk convs (3x3/s1/p1/d1, cin > 16, width a multiple of
+ * 48 or 64, height a multiple of 8, >= 256 tiles), else the two-barrier LDS-tiled 3x3 kernel where it
+ * applies (3x3, stride 1, pad == dilation in {1,2,4,8}, cin > 16, out >= 8x8, NHWC out), else the
+ * generic implicit-GEMM kernel; 1 = no pipelined kernel; 0 = generic kernel only; 3 = as 2 but the
+ * pipelined kernel at any tile count (tests). */
 int dbsr_set_conv_algo(int algo);
-/* Which kernel dbsr_conv2d would launch for `d` under the current selection: 1 LDS-tiled, 0 generic. */
+/* Which kernel dbsr_conv2d would launch for `d` under the current selection: 2 pipelined, 1 LDS-tiled,
+ * 0 generic. */
 int dbsr_conv_kernel_for(const dbsr_conv_desc* d);
 /* Scratch bytes dbsr_conv2d would use for split-K on `d` (0 = no split).  Convs whose grid cannot fill
  * the chip split K into slices that store fp32 partials to `workspace`; a second launch sums them in

@@ -62,8 +62,9 @@ def test_splitk_workspace_query(L):
 
 
 def test_packed_size(L):
-    # cin 117 -> 128 (cin > 16 pads to 32: 16 groups of 8) * 9 taps = 144 k-groups; cout 128 -> 128 rows
-    assert L.lib().dbsr_conv_packed_elems(128, 117, 3, 3) == 128 * 144 * 8
+    # cin 117 -> 128 (cin > 16 pads to 32: 16 groups of 8) * 9 taps = 144 k-groups; cout 128 -> 128 rows;
+    # 3x3 with cin > 16: followed by the chunk-major copy of the pipelined kernel (same size)
+    assert L.lib().dbsr_conv_packed_elems(128, 117, 3, 3) == 2 * 128 * 144 * 8
     # cin 4 -> 8 (1 group) * 9 taps = 9 -> 12 k-groups; cout 64
     assert L.lib().dbsr_conv_packed_elems(64, 4, 3, 3) == 64 * 12 * 8
     assert L.lib().dbsr_conv_packed_elems(3, 32, 1, 1) == 64 * 4 * 8

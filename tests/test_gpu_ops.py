@@ -132,7 +132,7 @@ def test_conv2d_tiled_vs_generic(ops, dtype, case):
     for algo in (1, 0):
         _lib.lib().dbsr_set_conv_algo(algo)
         outs.append(ops.conv2d(x, w, b, padding=1, act=1, residual=res, post_act=1, compute_dtype=dtype).float().cpu())
-    _lib.lib().dbsr_set_conv_algo(1)
+    _lib.lib().dbsr_set_conv_algo(2)
     # same products, fp32 accumulation, different summation order; outputs rounded to dtype
     tol = 1e-5 if dtype == torch.float32 else 1e-2
     np.testing.assert_allclose(outs[0].numpy(), outs[1].numpy(), atol=tol, rtol=tol)
@@ -158,3 +158,41 @@ def test_pwcnet_fixture(golden, synth_sd):
     with torch.no_grad():
         fl = pwc(torch.from_numpy(g['pwc_src']).to(DEV), torch.from_numpy(g['pwc_tgt']).to(DEV))
     np.testing.assert_allclose(fl.cpu().numpy(), g['pwc_flow'], atol=1e-3, rtol=0)
+
+
+PIPE_CASES = [   # N, Cin, H, W, Cout  (pipelined kernel configs: 64 x 48x8 and 32 x 64x8 tiles)
+    (2, 64, 48, 48, 64),        # encoder ResBlock shape, 2 chunks
+    (1, 192, 16, 48, 128),      # weight-predictor init: 6 chunks, 2 cout tiles
+    (1, 128, 8, 96, 80),        # partial cout tile (80 = 64 + 16)
+    (2, 32, 16, 128, 32),       # decoder post-ResBlock shape (1 chunk, 32-cout tiles)
+    (1, 40, 8, 64, 24),         # cin padded 40 -> 64, cout 24 < 32
+    (1, 64, 24, 64, 64),        # 64-wide, 64 couts: not a pipelined shape (falls back)
+]
+
+
+@pytest.mark.parametrize('case', PIPE_CASES)
+def test_conv2d_pipelined(ops, case):
+    """Pipelined persistent 3x3 kernel (algo 3 forces it) against the two-barrier tiled and generic
+    kernels and a torch fp32 conv on the same bf16-rounded operands."""
+    from dbsr_amd import _lib
+    N, Cin, H, W, Cout = case
+    gen = torch.Generator().manual_seed(Cin * 7 + Cout + H)
+    x = torch.randn(N, Cin, H, W, generator=gen)
+    w = torch.randn(Cout, Cin, 3, 3, generator=gen) / (Cin * 9) ** 0.5
+    b = torch.randn(Cout, generator=gen) * 0.1
+    res = torch.randn(N, Cout, H, W, generator=gen)
+    xb, wb, rb = (t.to(torch.bfloat16).float() for t in (x, w, res))
+    ref = F.relu(F.relu(F.conv2d(xb, wb, b, padding=1)) + rb)
+    outs = {}
+    try:
+        for algo in (3, 1, 0):
+            _lib.lib().dbsr_set_conv_algo(algo)
+            outs[algo] = ops.conv2d(x.to(DEV), w.to(DEV), b.to(DEV), padding=1, act=1, residual=res.to(DEV),
+                                    post_act=1, compute_dtype=torch.bfloat16).float().cpu()
+    finally:
+        _lib.lib().dbsr_set_conv_algo(2)
+    # bf16 outputs: one rounding of the fp32 sum (+ one of the pre-residual value) -> ~2^-8 relative
+    np.testing.assert_allclose(outs[3].numpy(), ref.numpy(), atol=3e-2, rtol=2e-2)
+    np.testing.assert_allclose(outs[3].numpy(), outs[1].numpy(), atol=3e-2, rtol=2e-2)
+    np.testing.assert_allclose(outs[3].numpy(), outs[0].numpy(), atol=3e-2, rtol=2e-2)
+    assert (outs[3] - ref).abs().mean() < 3e-3

@@ -28,7 +28,7 @@ def main():
     import argparse
     ap = argparse.ArgumentParser()
     ap.add_argument('--only', default=None, help='substring of the shape names to run')
-    ap.add_argument('--algos', default='1,0')
+    ap.add_argument('--algos', default='2,1,0')
     ap.add_argument('--reps', type=int, default=20)
     args = ap.parse_args()
     algos = [int(a) for a in args.algos.split(',')]
@@ -55,8 +55,8 @@ def main():
         for algo in algos:
             L.lib().dbsr_set_conv_algo(algo)
             ms = plan.time_ops(s, reps=args.reps)[0][1]
-            out.append('%s %7.1f us %6.1f TF/s' % ('tiled' if algo else 'generic', ms * 1e3, flop / ms / 1e9))
-        L.lib().dbsr_set_conv_algo(1)
+            out.append('%s %7.1f us %6.1f TF/s' % (['generic', 'tiled', 'auto', 'pipe'][algo], ms * 1e3, flop / ms / 1e9))
+        L.lib().dbsr_set_conv_algo(2)
         print(f'{name:22s} ' + ' | '.join(out))
 
 
