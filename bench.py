@@ -39,6 +39,7 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     ap.add_argument('--kernel-breakdown', action='store_true', help='print per-op device times to stderr')
+    ap.add_argument('--zero-flow', action='store_true', help='diagnostic: identity-flow stub instead of PWC-Net')
     return ap.parse_args()
 
 
@@ -85,6 +86,7 @@ def main():
     net = dbsr_amd.build_synthetic_net(seed=0).to(dev).eval()
     net.set_compute_dtype(dtype)
     net.use_graph = not args.no_graph
+    net.zero_flow = args.zero_flow
     B, N, S = args.batch, args.frames, args.size
     burst, _ = synthetic_bursts(B, N, S, S, sr_factor=8, seed=1000 + rank)
     burst = burst.to(dev)

@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get('DBSR_HIP_LIB', os.path.join(_HERE, 'libdbsr_hip.so'))
 DBSR_F32, DBSR_BF16 = 0, 1
 ACT_NONE, ACT_RELU, ACT_LRELU = 0, 1, 2
 OUT_NHWC, OUT_SHUFFLE, OUT_NCHW_F32 = 0, 1, 2
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 
 class FrameMap(ctypes.Structure):
@@ -40,7 +40,8 @@ class ConvDesc(ctypes.Structure):
                 ('act', ctypes.c_int),
                 ('res', Tensor), ('post_act', ctypes.c_int),
                 ('out_mode', ctypes.c_int), ('shuffle', ctypes.c_int),
-                ('workspace', ctypes.c_void_p), ('workspace_bytes', ctypes.c_size_t), ('precise', ctypes.c_int)]
+                ('workspace', ctypes.c_void_p), ('workspace_bytes', ctypes.c_size_t), ('precise', ctypes.c_int),
+                ('max_blocks', ctypes.c_int)]
 
 
 _lib = None

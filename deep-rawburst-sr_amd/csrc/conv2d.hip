@@ -44,6 +44,7 @@ struct ConvK {
     float* ws;         // [ksplit][npix][cw] fp32
     int cw;            // round_up(cout, 4)
     const void* w_pipe;  // chunk-major weight copy (3x3, cin > 16): [cout/16][chunk][tap][4 k-groups][16 co][8]
+    int max_blocks;      // persistent kernel: workgroup cap (0 = one per CU)
 };
 
 template <typename T> struct Frag;
@@ -932,7 +933,8 @@ int launch_pipe(const ConvK& k, int n_frames, hipStream_t s) {
         dbsr_set_error("conv2d: grid too large");
         return DBSR_E_ARG;
     }
-    int grid = (int)std::min<long long>(nt, num_cus());
+    const int cap = k.max_blocks > 0 ? std::min(k.max_blocks, num_cus()) : num_cus();
+    int grid = (int)std::min<long long>(nt, cap);
     grid = (grid + 7) / 8 * 8;
     // compile-time epilogues for the forward's three conv flavours, run-time otherwise
     int epi = 0;
@@ -1117,6 +1119,7 @@ ConvK make_convk(const dbsr_conv_desc* d) {
     k.ws = (float*)d->workspace;
     k.cw = round_up(d->cout, 4);
     k.w_pipe = (const char*)d->w + (size_t)round_up(d->cout, 64) * k.Kp * esz;
+    k.max_blocks = d->max_blocks;
     return k;
 }
 

@@ -25,6 +25,7 @@ Layout map (reference file:line per stage):
 """
 import ctypes
 import math
+import os
 
 import torch
 
@@ -107,7 +108,7 @@ class Plan:
     capture alike.
     """
     FORK, JOIN = '__fork__', '__join__'
-    MULTI_STREAM = True      # False: every lane runs on the caller's stream (debug / A-B timing)
+    MULTI_STREAM = os.environ.get('DBSR_SINGLE_STREAM', '0') != '1'   # False: every lane on the caller's stream
 
     def __init__(self):
         self.ops = []        # (callable | FORK | JOIN, args, name, lane)
@@ -118,6 +119,7 @@ class Plan:
         self.lane = 0
         self.lanes = {0}
         self.streams = {}
+        self.max_blocks = 0  # CU cap for lane-0 persistent convs issued while a side lane runs
 
     def add(self, name, fn, *args, work=None):
         if work is not None:
@@ -169,6 +171,7 @@ class Plan:
         d.out_mode, d.shuffle = out_mode, shuffle
         d.workspace, d.workspace_bytes = None, 0
         d.precise = 1 if precise else 0
+        d.max_blocks = self.max_blocks if self.lane == 0 else 0
         self.keep.append(d)
         self.convs.append((d, self.lane))
         flop = 2.0 * n_frames * oh * ow * pc.cout * d.cin * pc.kh * pc.kw
@@ -185,6 +188,8 @@ class Plan:
         for lane in sorted(self.lanes):
             ds = [d for d, ln in self.convs if ln == lane]
             need = max([L.lib().dbsr_conv_workspace_bytes(d) for d in ds] + [0])
+            if os.environ.get('DBSR_NO_SPLITK', '0') == '1':
+                need = 0                      # no scratch: every conv runs unsplit
             self.ws[lane] = torch.zeros(max(need // 4, 1), dtype=torch.float32, device=device)
             for d in ds:
                 d.workspace, d.workspace_bytes = self.ws[lane].data_ptr(), need
@@ -204,6 +209,38 @@ class Plan:
                 rc = fn(*args, stream if lane == 0 else self.streams[lane].cuda_stream)
                 if rc != 0:
                     L.check(rc, name)
+
+    def run_list(self, ops, stream):
+        """Launch `ops` (no fork/join entries) in order on one stream."""
+        for fn, args, name, lane in ops:
+            if fn is Plan.FORK or fn is Plan.JOIN:
+                continue
+            rc = fn(*args, stream)
+            if rc != 0:
+                L.check(rc, name)
+
+    def segments(self):
+        """(pre, side, main, post) op lists of a plan with one fork/join: lane-0 ops before the fork, the
+        side lane's ops, lane-0 ops between fork and join, ops after the join.  None if the plan has no
+        side lane."""
+        if not any(fn is Plan.FORK for fn, _, _, _ in self.ops):
+            return None
+        segs = {'pre': [], 'side': [], 'main': [], 'post': []}
+        state = 'pre'
+        for op in self.ops:
+            fn, args, name, lane = op
+            if fn is Plan.FORK:
+                assert state == 'pre', 'one fork per plan'
+                state = 'fork'
+                continue
+            if fn is Plan.JOIN:
+                state = 'post'
+                continue
+            if state == 'fork':
+                segs['side' if lane != 0 else 'main'].append(op)
+            else:
+                segs[state].append(op)
+        return segs['pre'], segs['side'], segs['main'], segs['post']
 
     def time_ops(self, stream, reps=10):
         """Average device time (ms) of each op, each launched `reps` times back to back between two
@@ -339,6 +376,8 @@ class PWCPlanner:
 # DBSR engine
 # ==================================================================================================
 class DBSREngine:
+    MAIN_FIRST = os.environ.get('DBSR_MAIN_FIRST', '1') == '1'
+
     def __init__(self, net):
         self.net = net
         self.dtype = net.compute_dtype
@@ -415,7 +454,9 @@ class DBSREngine:
         # Two lanes: the alignment chain (PWC-Net -> offsets -> offset-feature extractor, many small
         # latency-bound launches) runs on a high-priority side stream beside the per-frame encoder
         # (large launches); they meet at the warp.
-        plan.fork(1, dev, priority=-1)
+        plan.fork(1, dev, priority=int(os.environ.get('DBSR_SIDE_PRIO', '-1')))
+        # while the side lane runs, lane-0 persistent convs leave CUs to it (DBSR_LANE0_CUS, 0 = all)
+        plan_cap = int(os.environ.get('DBSR_LANE0_CUS', '0'))
         # ---------------- alignment (PWC-Net) ----------------
         if not zero_flow:
             flow_out = NHWC(P, Hp // 4, Wp // 4, 2, torch.float32, dev)
@@ -446,6 +487,7 @@ class DBSREngine:
         if not self.ofe_res:
             raise NotImplementedError('num_offset_feat_extractor_res must be >= 1')
         plan.switch(0)
+        plan.max_blocks = plan_cap
         # ---------------- encoder (encoders.py:66-72) ----------------
         e = [NHWC(F, H, W, r8(self.enc_init.cout), dt, dev) for _ in range(3)]
         plan.conv('enc.init', self.enc_init, F, raw, 0, hw, e[0], 0, L.ACT_RELU)
@@ -456,6 +498,7 @@ class DBSREngine:
         PJ = NHWC(F, H, W, r8(pd), dt, dev)
         plan.conv('merge.proj_ref', self.proj, B, E, 0, hw, PJ, 0, L.ACT_RELU, xmap=(1, N, 0, 1), ymap=(1, N, 0, 1))
         plan.join(1)
+        plan.max_blocks = 0
         # ---------------- warp (encoders.py:80) ----------------
         Wf = NHWC(max(P, 1), H, W, C, dt, dev)
         es = 2 if dt == torch.bfloat16 else 4
@@ -506,6 +549,57 @@ class DBSREngine:
         plan.shape = (B, N, H, W)
         return plan
 
+    @staticmethod
+    def _capture(plan, dev):
+        """HIP graph(s) of a plan.  Default: one graph.  Its replay puts every kernel node on ONE hardware
+        queue (rocprofv3 trace), independent nodes without a barrier between them.  DBSR_LANE_GRAPHS=1
+        captures a plan with a side lane as four single-stream graphs instead -- pre (burst packing), side
+        (PWC-Net + offset features), main (encoder), post (after the join) -- replayed on two streams, so
+        the lanes sit on two queues; measured 1-3 % slower at cfg2 (each replay pays ~10 us of host time
+        per node, so the ~100-node side graph delays whatever is submitted after it)."""
+        segs = plan.segments() if os.environ.get('DBSR_LANE_GRAPHS', '0') == '1' else None
+        if segs is None:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                plan.run(L.stream_ptr(dev))
+            return g
+        side = plan.streams[1]
+        main = torch.cuda.Stream(device=dev)
+        out = []
+        for ops, st in zip(segs, (main, side, main, main)):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=st):
+                plan.run_list(ops, st.cuda_stream)
+            out.append(g)
+        return tuple(out) + (torch.cuda.Event(), torch.cuda.Event())
+
+    @staticmethod
+    def _replay(plan, g):
+        if not isinstance(g, tuple):
+            g.replay()
+            return
+        g_pre, g_side, g_main, g_post, ev_fork, ev_join = g
+        cur = torch.cuda.current_stream()
+        side = plan.streams[1]
+        g_pre.replay()
+        ev_fork.record(cur)
+        side.wait_event(ev_fork)
+        # Submission order matters: a replay's host cost grows with its node count (the side graph has
+        # ~100 short kernels), and the next replay call waits for it.  The main lane's few long encoder
+        # kernels are submitted first so they start at once; the side lane's kernels then stream in
+        # while the encoder runs.
+        if DBSREngine.MAIN_FIRST:
+            g_main.replay()
+            with torch.cuda.stream(side):
+                g_side.replay()
+        else:
+            with torch.cuda.stream(side):
+                g_side.replay()
+            g_main.replay()
+        ev_join.record(side)
+        cur.wait_event(ev_join)
+        g_post.replay()
+
     def _set_fw(self, plan, want):
         fn, args, name, lane = plan.ops[plan.fuse_idx]
         args = list(plan.fuse_args)
@@ -536,11 +630,9 @@ class DBSREngine:
             g = self.graphs.get((key, want_fw))
             if g is None:
                 plan.run(stream)                      # warm-up outside capture
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
-                    plan.run(L.stream_ptr(dev))
+                g = self._capture(plan, dev)
                 self.graphs[(key, want_fw)] = g
-            g.replay()
+            self._replay(plan, g)
             pred, offs = plan.bufs['pred'], plan.bufs['offsets']
             fw_t = plan.FW.t
         else:

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define DBSR_ABI_VERSION 1
+#define DBSR_ABI_VERSION 2
 
 enum { DBSR_F32 = 0, DBSR_BF16 = 1 };
 enum { DBSR_ACT_NONE = 0, DBSR_ACT_RELU = 1, DBSR_ACT_LRELU = 2 };      /* LeakyReLU slope 0.1 */
@@ -80,6 +80,8 @@ typedef struct dbsr_conv_desc {
     void* workspace;                  /* optional fp32 scratch for split-K (may be NULL) */
     size_t workspace_bytes;
     int precise;                      /* 1: bf16 activations x fp32-packed weights on fp32 MFMA (fp32 out) */
+    int max_blocks;                   /* > 0: cap on the persistent kernel's workgroups (CUs it occupies),
+                                         leaving the rest of the chip to concurrent streams; 0 = all CUs */
 } dbsr_conv_desc;
 
 /* Packed weight layout: [cout_pad][kgp*8] with k-group kg = (ky*kw+kx)*(cinp/8) + c/8, where
