@@ -16,6 +16,7 @@ import sys
 KERNELS = {   # label -> (name predicate, algorithmic bytes per launch at the default bench workload)
     'warp_kernel (DBSR warp, encoders.py:80)': (lambda n: ('warp_kernel' in n and 'backwarp' not in n) or 'warp512_bf16_kernel' in n, None),
     'fuse_softmax_kernel (merging.py:116-126)': (lambda n: 'fuse_softmax_kernel' in n, None),
+    'conv3x3_pipe_kernel, largest grid (wp.out 128->512)': (lambda n: 'conv3x3_pipe_kernel<64, 48, 8, 3>' in n, None),
 }
 
 
