@@ -375,8 +375,29 @@ class PWCPlanner:
 # ==================================================================================================
 # DBSR engine
 # ==================================================================================================
+def cu_mask_stream(device, cus):
+    """A HIP stream whose kernels may only run on the CUs in `cus` (hipExtStreamCreateWithCUMask), as a
+    torch ExternalStream."""
+    hip = ctypes.CDLL('libamdhip64.so')
+    n = torch.cuda.get_device_properties(device).multi_processor_count
+    words = (n + 31) // 32
+    mask = (ctypes.c_uint32 * words)()
+    for c in cus:
+        mask[c // 32] |= 1 << (c % 32)
+    sp = ctypes.c_void_p()
+    with torch.cuda.device(device):
+        rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(sp), ctypes.c_uint32(words), mask)
+    if rc != 0:
+        raise RuntimeError('hipExtStreamCreateWithCUMask failed: %d' % rc)
+    return torch.cuda.ExternalStream(sp.value, device=device)
+
+
 class DBSREngine:
     MAIN_FIRST = os.environ.get('DBSR_MAIN_FIRST', '1') == '1'
+    LANE_GRAPHS = os.environ.get('DBSR_LANE_GRAPHS', '0') == '1'
+    # CUs reserved for the side lane (PWC-Net) while the encoder runs: the lanes then run on disjoint
+    # CU sets (hipExtStreamCreateWithCUMask) instead of contending for the same CUs; 0 = shared
+    CU_SPLIT = int(os.environ.get('DBSR_CU_SPLIT', '0'))
 
     def __init__(self, net):
         self.net = net
@@ -457,6 +478,14 @@ class DBSREngine:
         plan.fork(1, dev, priority=int(os.environ.get('DBSR_SIDE_PRIO', '-1')))
         # while the side lane runs, lane-0 persistent convs leave CUs to it (DBSR_LANE0_CUS, 0 = all)
         plan_cap = int(os.environ.get('DBSR_LANE0_CUS', '0'))
+        if DBSREngine.CU_SPLIT:
+            n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
+            k = DBSREngine.CU_SPLIT
+            # every (n_cu // k)-th CU to the side lane: spread over XCDs / shader engines
+            side_cus = [c for c in range(n_cu) if c % (n_cu // k) == 0][:k]
+            main_cus = [c for c in range(n_cu) if c not in set(side_cus)]
+            plan.cu_streams = (cu_mask_stream(dev, main_cus), cu_mask_stream(dev, side_cus))
+            plan_cap = len(main_cus)
         # ---------------- alignment (PWC-Net) ----------------
         if not zero_flow:
             flow_out = NHWC(P, Hp // 4, Wp // 4, 2, torch.float32, dev)
@@ -557,46 +586,49 @@ class DBSREngine:
         (PWC-Net + offset features), main (encoder), post (after the join) -- replayed on two streams, so
         the lanes sit on two queues; measured 1-3 % slower at cfg2 (each replay pays ~10 us of host time
         per node, so the ~100-node side graph delays whatever is submitted after it)."""
-        segs = plan.segments() if os.environ.get('DBSR_LANE_GRAPHS', '0') == '1' else None
+        segs = plan.segments() if (DBSREngine.LANE_GRAPHS or DBSREngine.CU_SPLIT) else None
         if segs is None:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 plan.run(L.stream_ptr(dev))
             return g
-        side = plan.streams[1]
-        main = torch.cuda.Stream(device=dev)
+        if DBSREngine.CU_SPLIT:
+            main_s, side_s = plan.cu_streams
+        else:
+            main_s, side_s = torch.cuda.Stream(device=dev), plan.streams[1]
+        other = torch.cuda.Stream(device=dev)
         out = []
-        for ops, st in zip(segs, (main, side, main, main)):
+        for ops, st in zip(segs, (other, side_s, main_s, other)):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=st):
                 plan.run_list(ops, st.cuda_stream)
             out.append(g)
-        return tuple(out) + (torch.cuda.Event(), torch.cuda.Event())
+        return tuple(out) + (main_s, side_s, torch.cuda.Event(), torch.cuda.Event(), torch.cuda.Event())
 
     @staticmethod
     def _replay(plan, g):
         if not isinstance(g, tuple):
             g.replay()
             return
-        g_pre, g_side, g_main, g_post, ev_fork, ev_join = g
+        g_pre, g_side, g_main, g_post, main_s, side_s, ev_fork, ev_main, ev_join = g
         cur = torch.cuda.current_stream()
-        side = plan.streams[1]
         g_pre.replay()
         ev_fork.record(cur)
-        side.wait_event(ev_fork)
+        side_s.wait_event(ev_fork)
+        main_s.wait_event(ev_fork)
         # Submission order matters: a replay's host cost grows with its node count (the side graph has
         # ~100 short kernels), and the next replay call waits for it.  The main lane's few long encoder
         # kernels are submitted first so they start at once; the side lane's kernels then stream in
         # while the encoder runs.
-        if DBSREngine.MAIN_FIRST:
-            g_main.replay()
-            with torch.cuda.stream(side):
-                g_side.replay()
-        else:
-            with torch.cuda.stream(side):
-                g_side.replay()
-            g_main.replay()
-        ev_join.record(side)
+        order = [(main_s, g_main), (side_s, g_side)]
+        if not DBSREngine.MAIN_FIRST:
+            order.reverse()
+        for st, gg in order:
+            with torch.cuda.stream(st):
+                gg.replay()
+        ev_main.record(main_s)
+        ev_join.record(side_s)
+        cur.wait_event(ev_main)
         cur.wait_event(ev_join)
         g_post.replay()
 
