@@ -149,10 +149,14 @@ def main():
                       'frac': round(gbs / PEAK_HBM_GBS, 4), 'traffic': None, 'us': round(ms * 1e3, 2),
                       'alg_bytes': by}
     if args.kernel_breakdown and rank == 0:
-        for name, ms in times:
+        for i, (name, ms) in enumerate(times):
             if name.startswith('sync.'):
                 continue
-            print(f'{name:32s} {ms * 1e3:9.1f} us', file=sys.stderr)
+            kind = plan.kernel.get(i) or '-'
+            w = plan.work[i][1] if i in plan.work else 0.0
+            rate = '%8.1f %s' % ((w / (ms * 1e-3) / 1e12, 'TF/s') if kind.startswith('conv') else
+                                 (w / (ms * 1e-3) / 1e9, 'GB/s')) if (w and ms) else ''
+            print(f'{name:32s} {ms * 1e3:9.1f} us  {kind:15s} {rate}', file=sys.stderr)
         for k, (ms, w, n) in sorted(fam.items(), key=lambda kv: -kv[1][0]):
             print(f'[family] {k:12s} {ms * 1e3:9.1f} us  n={n}', file=sys.stderr)
         print(f'sum of op times {sum(t for _, t in times) * 1e3:.1f} us vs step {ms_step * 1e3:.1f} us',

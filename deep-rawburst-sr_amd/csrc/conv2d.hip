@@ -45,6 +45,9 @@ struct ConvK {
     int cw;            // round_up(cout, 4)
     const void* w_pipe;  // chunk-major weight copy (3x3, cin > 16): [cout/16][chunk][tap][4 k-groups][16 co][8]
     int max_blocks;      // persistent kernel: workgroup cap (0 = one per CU)
+    const float* head_w; // fused 1x1 head (pipelined kernel, EPI 4): fp32 [head_cout][cout], bias [head_cout]
+    const float* head_b;
+    int head_cout;       // y is then the head's fp32 NCHW output (y_is = image stride)
 };
 
 template <typename T> struct Frag;
@@ -688,21 +691,30 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pipe_kernel(ConvK k, int tiles
     const int g = lane >> 4, col = lane & 15;
     const int nchunks = k.CG / 4;
     // epilogue variants (compile-time where the forward's convs need them): 1 act(ReLU), 2 conv + residual
-    // then ReLU (ResBlock conv2), 3 plain; 0 reads act / residual / post_act at run time
-    const bool has_res = EPI == 2 || (EPI == 0 && k.r != nullptr);
+    // then ReLU (ResBlock conv2), 3 plain, 4 as 2 followed by a 1x1 head (<= 4 outputs) + ReLU whose fp32
+    // NCHW result is the only thing stored (the decoder's last ResBlock + RGB predictor, decoders.py:59-61);
+    // 0 reads act / residual / post_act at run time
+    constexpr bool HEAD = EPI == 4;
+    static_assert(!HEAD || WM == 32, "the head reads all 32 channels of a pixel from one cout tile");
+    const bool has_res = EPI == 2 || HEAD || (EPI == 0 && k.r != nullptr);
     auto act1 = [&](float v) {
         if constexpr (EPI == 1) return fmaxf(v, 0.f);
         else if constexpr (EPI == 0) return apply_act(v, k.act);
         else return v;
     };
     auto act2 = [&](float v) {
-        if constexpr (EPI == 2) return fmaxf(v, 0.f);
+        if constexpr (EPI == 2 || EPI == 4) return fmaxf(v, 0.f);
         else if constexpr (EPI == 0) return apply_act(v, k.post_act);
         else return v;
     };
 
     // bias into LDS once; ordered before its first read by the loop's first barrier
     for (int c = threadIdx.x; c < nct * WM; c += 512) lbias[c] = (k.bias && c < k.cout) ? k.bias[c] : 0.f;
+    float* lhead = lbias + 256;                          // HEAD: weights [4][32] at +256, bias [4] at +384
+    if constexpr (HEAD) {
+        if (threadIdx.x < 128) lhead[threadIdx.x] = threadIdx.x < k.head_cout * 32 ? k.head_w[threadIdx.x] : 0.f;
+        if (threadIdx.x < 4) lhead[128 + threadIdx.x] = (k.head_b && (int)threadIdx.x < k.head_cout) ? k.head_b[threadIdx.x] : 0.f;
+    }
 
     // persistent tile walk, XCD-grouped: the blocks sharing an XCD (equal blockIdx % 8) take a
     // contiguous range of tile ids per round, so a spatial tile's cout tiles and neighbouring halos
@@ -725,7 +737,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pipe_kernel(ConvK k, int tiles
         t.y0 = ty * TH; t.x0 = tx * TW; t.cb = ct * WM;
         t.xf = (const T*)k.x + map_frame(k.xm, f) * k.x_is;
         const long long pix = (long long)t.y0 * k.out_w + t.x0;
-        t.y_off = map_frame(k.ym, f) * k.y_is + k.y_c0 + t.cb + pix * k.y_ld;
+        t.y_off = HEAD ? map_frame(k.ym, f) * k.y_is + pix : map_frame(k.ym, f) * k.y_is + k.y_c0 + t.cb + pix * k.y_ld;
         t.r_off = has_res ? map_frame(k.rm, f) * k.r_is + k.r_c0 + t.cb + pix * k.r_ld : 0;
         return t;
     };
@@ -807,8 +819,28 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pipe_kernel(ConvK k, int tiles
                 }
             }
             u32x4_t o;
+            if constexpr (HEAD) {
+                // lane (g, col) holds channels 8g..8g+7 of its pixel: partial head sums, reduced over the
+                // four g lanes of the column (xor 16, 32); lane g then keeps output channel g
+                float hs[4];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) o[e] = pack_bf16x2(v[2 * e], v[2 * e + 1]);
+                for (int c = 0; c < 4; ++c) {
+                    const float4 w0 = *(const float4*)(lhead + c * 32 + 8 * g);
+                    const float4 w1 = *(const float4*)(lhead + c * 32 + 8 * g + 4);
+                    float a = v[0] * w0.x;
+                    a = fmaf(v[1], w0.y, a); a = fmaf(v[2], w0.z, a); a = fmaf(v[3], w0.w, a);
+                    a = fmaf(v[4], w1.x, a); a = fmaf(v[5], w1.y, a); a = fmaf(v[6], w1.z, a); a = fmaf(v[7], w1.w, a);
+                    a += __shfl_xor(a, 16, 64);
+                    a += __shfl_xor(a, 32, 64);
+                    hs[c] = a;
+                }
+                const float hv = g == 0 ? hs[0] : g == 1 ? hs[1] : g == 2 ? hs[2] : hs[3];
+                o[0] = __float_as_uint(fmaxf(hv + lhead[128 + g], 0.f));
+                o[1] = o[2] = o[3] = 0u;
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) o[e] = pack_bf16x2(v[2 * e], v[2 * e + 1]);
+            }
             pend[q] = o;
             acc[2 * h][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
             acc[2 * h + 1][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
@@ -816,7 +848,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pipe_kernel(ConvK k, int tiles
     };
     auto store_piece = [&](int q, const Tile& t) {   // runs of couts >= cout (partial cout tile) skipped
         const int h = q / C::GW, j = q % C::GW;
-        if (t.cb + 32 * h + 8 * g < k.cout)
+        if constexpr (HEAD) {
+            // NCHW fp32: lanes of one g write 16 consecutive pixels of plane g
+            if (g < k.head_cout)
+                ((float*)k.y)[t.y_off + (long long)wave * C::RPW * k.out_w + col + grp_off(j) +
+                              (long long)g * k.out_h * k.out_w] = __uint_as_float(pend[q][0]);
+        } else if (t.cb + 32 * h + 8 * g < k.cout)
             *(u32x4_t*)((T*)k.y + t.y_off + y_lane + grp_off(j) * k.y_ld + 32 * h) = pend[q];
     };
 
@@ -938,13 +975,17 @@ int launch_pipe(const ConvK& k, int n_frames, hipStream_t s) {
     grid = (grid + 7) / 8 * 8;
     // compile-time epilogues for the forward's three conv flavours, run-time otherwise
     int epi = 0;
-    if (!k.r && k.act == DBSR_ACT_RELU) epi = 1;
+    if (k.head_cout > 0) epi = 4;
+    else if (!k.r && k.act == DBSR_ACT_RELU) epi = 1;
     else if (k.r && k.act == DBSR_ACT_NONE && k.post_act == DBSR_ACT_RELU) epi = 2;
     else if (!k.r && k.act == DBSR_ACT_NONE) epi = 3;
 #define DBSR_PIPE_LAUNCH(E)                                                                                    \
     hipLaunchKernelGGL((conv3x3_pipe_kernel<WM, TW, TH, E>), dim3(grid), dim3(512), 0, s, k, tiles_x, tiles_y, \
                        nct, (int)nt)
     switch (epi) {
+        case 4:
+            if constexpr (WM == 32) DBSR_PIPE_LAUNCH(4);
+            break;
         case 1: DBSR_PIPE_LAUNCH(1); break;
         case 2: DBSR_PIPE_LAUNCH(2); break;
         case 3: DBSR_PIPE_LAUNCH(3); break;
@@ -1120,6 +1161,7 @@ ConvK make_convk(const dbsr_conv_desc* d) {
     k.cw = round_up(d->cout, 4);
     k.w_pipe = (const char*)d->w + (size_t)round_up(d->cout, 64) * k.Kp * esz;
     k.max_blocks = d->max_blocks;
+    k.head_w = nullptr; k.head_b = nullptr; k.head_cout = 0;
     return k;
 }
 
@@ -1129,6 +1171,11 @@ extern "C" int dbsr_conv_kernel_for(const dbsr_conv_desc* d) {
     if (!d) return -1;
     if (pick_pipe(d)) return 2;
     return use_tiled(d) ? 1 : 0;
+}
+
+extern "C" int dbsr_conv_head_ok(const dbsr_conv_desc* d) {
+    return d && pick_pipe(d) == 2 && d->cout == 32 && d->res.ptr && d->act == DBSR_ACT_NONE &&
+           d->post_act == DBSR_ACT_RELU;
 }
 
 extern "C" size_t dbsr_conv_workspace_bytes(const dbsr_conv_desc* d) {
@@ -1217,6 +1264,22 @@ extern "C" int dbsr_conv2d(const dbsr_conv_desc* d, void* stream) {
         return launch_conv<float, 1, 1, bf16_t>(k, s);
     }
     return d->x.dtype == DBSR_BF16 ? dispatch_conv<bf16_t>(k, d, s) : dispatch_conv<float>(k, d, s);
+}
+
+extern "C" int dbsr_conv2d_head(const dbsr_conv_desc* d, const float* head_w, const float* head_b, int head_cout,
+                                dbsr_tensor head_out, void* stream) {
+    DBSR_CHECK_ARG(d && head_w && head_out.ptr, "conv2d_head: null pointer");
+    DBSR_CHECK_ARG(dbsr_conv_head_ok(d), "conv2d_head: the conv must be a pipelined 32-channel ResBlock conv2 "
+                   "(bf16 3x3/s1/p1, residual, act none, post-act ReLU, width %% 64 == 0, height %% 8 == 0)");
+    DBSR_CHECK_ARG(head_cout >= 1 && head_cout <= 4, "conv2d_head: head_cout must be 1..4");
+    DBSR_CHECK_ARG(head_out.dtype == DBSR_F32 && head_out.map.fpg > 0, "conv2d_head: fp32 NCHW output");
+    DBSR_CHECK_ARG(d->x.ld % 8 == 0 && d->x.c0 % 8 == 0 && d->x.c0 + cin_pad(d->cin) <= d->x.ld,
+                   "conv2d_head: bad input slice");
+    DBSR_CHECK_ARG(d->res.dtype == DBSR_BF16 && d->res.map.fpg > 0, "conv2d_head: residual must be bf16");
+    ConvK k = make_convk(d);
+    k.head_w = head_w; k.head_b = head_b; k.head_cout = head_cout;
+    k.y = head_out.ptr; k.y_f32 = 1; k.y_is = head_out.img_stride; k.y_ld = 1; k.y_c0 = 0; k.ym = head_out.map;
+    return launch_pipe<32, 64, 8>(k, d->n_frames, (hipStream_t)stream);
 }
 
 #ifdef DBSR_PIPE_STAMPS

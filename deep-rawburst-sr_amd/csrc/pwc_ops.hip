@@ -94,16 +94,19 @@ __global__ void backwarp_kernel(int n, int h, int w, int C, dbsr_tensor in, dbsr
 // ------------------------------------------------------------------------------------------------
 // ConvTranspose2d(k=4, s=2, p=1) (pwcnet.py:119-120): out[oy,ox,co] = b[co] + sum over the 2x2 input
 // pixels iy=(oy+1-ky)/2, ix=(ox+1-kx)/2 and all ci of in[iy,ix,ci]*w[ci,co,ky,kx].
-// Weights repacked as [ky][kx][co][cin8] (zero-padded to a multiple of 8 channels) so a wave reads
-// them contiguously; one wave per output pixel, lane = 8-channel group, shuffle reduction.
+// Weights repacked as [ky][kx][co][cin8] (zero-padded to a multiple of 8 channels) so a lane group
+// reads them contiguously.  SG lanes per output pixel (lane = 8-channel group, shuffle reduction over
+// the group): SG = 1 for the 2-channel upflow (a thread per pixel, no idle lanes), 32 for the ~70
+// groups of the upfeat inputs (two pixels per wave, ~2 groups per lane).
 // ------------------------------------------------------------------------------------------------
-template <typename T>
+template <typename T, int SG>
 __global__ __launch_bounds__(256) void convt_k4s2_kernel(int n, int h, int w, int cin8, int cout, dbsr_tensor in,
                                                          const float* __restrict__ wgt, const float* __restrict__ bias,
                                                          dbsr_tensor out, int vec) {
-    const int lane = threadIdx.x & 63;
-    const long long opix = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int sl = threadIdx.x & (SG - 1);
+    const long long opix = (long long)blockIdx.x * (256 / SG) + threadIdx.x / SG;
     const int H2 = 2 * h, W2 = 2 * w;
+    // whole lane groups leave together (the shuffle below stays within a group)
     if (opix >= (long long)n * H2 * W2) return;
     const int p = (int)(opix / (H2 * W2));
     const int rr = (int)(opix - (long long)p * H2 * W2);
@@ -120,7 +123,7 @@ __global__ __launch_bounds__(256) void convt_k4s2_kernel(int n, int h, int w, in
             if (ix < 0 || ix >= w) continue;
             const T* src = base + ((long long)iy * w + ix) * in.ld;
             const float* wt = wgt + (long long)((ky * 4 + kx) * cout) * cin8;
-            for (int cgi = lane; cgi < ngroups; cgi += 64) {
+            for (int cgi = sl; cgi < ngroups; cgi += SG) {
                 float v[8];
                 if (vec) {
                     load8(src + cgi * 8, v);
@@ -143,10 +146,11 @@ __global__ __launch_bounds__(256) void convt_k4s2_kernel(int n, int h, int w, in
 #pragma unroll
     for (int co = 0; co < 4; ++co) {
         float v = acc[co];
-        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+#pragma unroll
+        for (int off = SG / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
         acc[co] = v;
     }
-    if (lane == 0) {
+    if (sl == 0) {
         float* o = img_ptr<float>(out, p) + (long long)rr * out.ld;
         for (int co = 0; co < cout; ++co) o[co] = acc[co] + (bias ? bias[co] : 0.f);
     }
@@ -336,8 +340,16 @@ extern "C" int dbsr_conv_transpose_k4s2(int n, int h, int w, int cin, int cout, 
     const long long opix = (long long)n * 4 * h * w;
     return by_dtype(in.dtype, [&](auto* tag) {
         using T = std::remove_pointer_t<decltype(tag)>;
-        hipLaunchKernelGGL(convt_k4s2_kernel<T>, dim3(nblocks(opix, 4)), dim3(256), 0, (hipStream_t)stream, n, h, w,
-                           cin8, cout, in, wgt, bias, out, vec);
+        const int ng = cin8 / 8;
+#define DBSR_CONVT(SG)                                                                                              \
+    hipLaunchKernelGGL((convt_k4s2_kernel<T, SG>), dim3(nblocks(opix, 256 / SG)), dim3(256), 0, (hipStream_t)stream, \
+                       n, h, w, cin8, cout, in, wgt, bias, out, vec)
+        if (ng <= 1) DBSR_CONVT(1);
+        else if (ng <= 8) DBSR_CONVT(4);
+        else if (ng <= 24) DBSR_CONVT(8);
+        else if (ng <= 96) DBSR_CONVT(32);
+        else DBSR_CONVT(64);
+#undef DBSR_CONVT
         DBSR_LAUNCH_CHECK();
         return 0;
     });

@@ -152,7 +152,10 @@ class Plan:
 
     def conv(self, name, pc, n_frames, x, xc0, in_hw, y, yc0, act, xmap=IDENTITY, ymap=IDENTITY, res=None,
              rc0=0, rmap=IDENTITY, post_act=L.ACT_NONE, out_mode=L.OUT_NHWC, shuffle=0, y_desc=None, cin=None,
-             precise=False):
+             precise=False, head=None):
+        """Emit one conv.  head = (name, w [hc, cout] fp32, b [hc] | None, out_desc): when the library can fuse
+        it (dbsr_conv_head_ok), the conv's own output is not stored and the 1x1 head + ReLU writes out_desc
+        (fp32 NCHW); the returned desc then has .fused_head = True."""
         oh, ow = pc.out_hw(*in_hw)
         assert cin is None or cin == pc.cin, (name, cin, pc.cin)
         d = L.ConvDesc()
@@ -175,6 +178,15 @@ class Plan:
         self.keep.append(d)
         self.convs.append((d, self.lane))
         flop = 2.0 * n_frames * oh * ow * pc.cout * d.cin * pc.kh * pc.kw
+        d.fused_head = bool(head is not None and L.lib().dbsr_conv_head_ok(ctypes.byref(d)))
+        if d.fused_head:
+            hname, hw, hb, hdesc = head
+            self.keep.extend([hw, hb, hdesc])
+            flop += 2.0 * n_frames * oh * ow * hw.shape[0] * hw.shape[1]
+            self.add(name + '+' + hname, L.lib().dbsr_conv2d_head, ctypes.byref(d), hw.data_ptr(),
+                     hb.data_ptr() if hb is not None else None, hw.shape[0], hdesc, work=('flop', flop))
+            self.kernel[len(self.ops) - 1] = 'conv3x3_pipe'
+            return d
         self.add(name, L.lib().dbsr_conv2d, ctypes.byref(d), work=('flop', flop))
         self.kernel[len(self.ops) - 1] = {2: 'conv3x3_pipe', 1: 'conv3x3_tiled'}.get(L.lib().dbsr_conv_kernel_for(d),
                                                                                       'conv2d_generic')
@@ -398,6 +410,8 @@ class DBSREngine:
     # CUs reserved for the side lane (PWC-Net) while the encoder runs: the lanes then run on disjoint
     # CU sets (hipExtStreamCreateWithCUMask) instead of contending for the same CUs; 0 = shared
     CU_SPLIT = int(os.environ.get('DBSR_CU_SPLIT', '0'))
+    # bf16: fuse the RGB predictor into the last decoder ResBlock conv (DBSR_FUSED_HEAD=0: separate kernel)
+    FUSED_HEAD = os.environ.get('DBSR_FUSED_HEAD', '1') == '1'
 
     def __init__(self, net):
         self.net = net
@@ -439,20 +453,27 @@ class DBSREngine:
         # the RGB predictor runs fp32 math on bf16 features (0.2 GFLOP/burst; removes ~40 % of the bf16
         # PSNR delta, tools/bf16_sensitivity.py)
         self.pred = PackedConv(dec.predictor[0], torch.float32, device, stream)
+        pm = dec.predictor[0]
+        self.head_w = pm.weight.detach().to(device=device, dtype=torch.float32).reshape(pm.out_channels, -1).contiguous()
+        self.head_b = (pm.bias.detach().to(device=device, dtype=torch.float32).contiguous()
+                       if pm.bias is not None else None)
         self.device = device
         self.sig = _param_signature(net)
         self.plans, self.graphs = {}, {}
 
-    def _resblocks(self, plan, name, blocks, n, hw, bufs, x_idx, dtype):
-        """ResBlock chain (blocks.py:81-96) over ping-pong buffers; returns index of the result buffer."""
+    def _resblocks(self, plan, name, blocks, n, hw, bufs, x_idx, dtype, head=None):
+        """ResBlock chain (blocks.py:81-96) over ping-pong buffers; returns index of the result buffer
+        (and, with `head`, whether the head got fused into the last conv -- see Plan.conv)."""
         a = x_idx
+        fused = False
         for i, (c1, c2) in enumerate(blocks):
             b, c = [j for j in range(3) if j != a]
             plan.conv(f'{name}{i}.conv1', c1, n, bufs[a], 0, hw, bufs[b], 0, L.ACT_RELU)
-            plan.conv(f'{name}{i}.conv2', c2, n, bufs[b], 0, hw, bufs[c], 0, L.ACT_NONE, res=bufs[a],
-                      post_act=L.ACT_RELU)
+            d = plan.conv(f'{name}{i}.conv2', c2, n, bufs[b], 0, hw, bufs[c], 0, L.ACT_NONE, res=bufs[a],
+                          post_act=L.ACT_RELU, head=head if i == len(blocks) - 1 else None)
+            fused = d.fused_head
             a = c
-        return a
+        return (a, fused) if head is not None else a
 
     def _build(self, B, N, H, W):
         dt, dev = self.dtype, self.device
@@ -564,11 +585,20 @@ class DBSREngine:
             plan.keep.append(kbuf)
             plan.add('dec.blur', lib.dbsr_gauss_blur3, B, H * S, W * S, pc, sh[0].d(0), kbuf, sh[1].d(0))
             a = 1
-        i = self._resblocks(plan, 'dec.post', self.dec_post, B, (H * S, W * S), sh, a, dt)
         bufs['pred'] = torch.zeros(B, 3, H * S, W * S, dtype=torch.float32, device=dev)
         pdesc = L.tensor_desc(bufs['pred'], 1, 0, img_stride=3 * H * S * W * S, dtype=torch.float32)
-        plan.conv('dec.predictor', self.pred, B, sh[i], 0, (H * S, W * S), None, 0, L.ACT_RELU,
-                  out_mode=L.OUT_NCHW_F32, y_desc=pdesc, precise=(dt == torch.bfloat16))
+        # bf16: the last post ResBlock's conv2 and the RGB predictor in one kernel (its 32-channel output
+        # never reaches HBM; the head runs fp32 on the fp32 ResBlock output, decoders.py:59-61)
+        head = None
+        if dt == torch.bfloat16 and self.dec_post and DBSREngine.FUSED_HEAD:
+            head = ('predictor', self.head_w, self.head_b, pdesc)
+        if head is not None:
+            i, fused = self._resblocks(plan, 'dec.post', self.dec_post, B, (H * S, W * S), sh, a, dt, head=head)
+        else:
+            i, fused = self._resblocks(plan, 'dec.post', self.dec_post, B, (H * S, W * S), sh, a, dt), False
+        if not fused:
+            plan.conv('dec.predictor', self.pred, B, sh[i], 0, (H * S, W * S), None, 0, L.ACT_RELU,
+                      out_mode=L.OUT_NCHW_F32, y_desc=pdesc, precise=(dt == torch.bfloat16))
         plan.keep.extend([raw, rgb, om, e, E, Wf, PJ, WP, o, q, LG, FUS, FW, g, sh])
         plan.finalize_workspace(dev)
         plan.bufs = bufs

@@ -79,8 +79,10 @@ def warp(feat, flow, mode='bilinear', padding_mode='zeros'):
 
 
 def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, act=L.ACT_NONE, residual=None,
-           post_act=L.ACT_NONE, compute_dtype=torch.float32, out_f32=False):
-    """act(conv2d(x) + bias) (+ residual, then post_act); NCHW in/out, computed by dbsr_conv2d."""
+           post_act=L.ACT_NONE, compute_dtype=torch.float32, out_f32=False, head=None):
+    """act(conv2d(x) + bias) (+ residual, then post_act); NCHW in/out, computed by dbsr_conv2d.
+    head = (w [hc, Cout, 1, 1], b [hc] | None): return ReLU(conv1x1(result, w, b)) as fp32 NCHW instead,
+    computed by dbsr_conv2d_head (the conv's own result is not stored)."""
     _need_cuda(x, weight)
     N, Cin, H, W = x.shape
     Cout, _, kh, kw = weight.shape
@@ -120,5 +122,15 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, act=L.ACT_NONE
     need = L.lib().dbsr_conv_workspace_bytes(d)
     ws = torch.zeros(max(need // 4, 1), dtype=torch.float32, device=dev)
     d.workspace, d.workspace_bytes = ws.data_ptr(), need
+    if head is not None:
+        hw, hb = head
+        hc = hw.shape[0]
+        hw32 = hw.reshape(hc, -1).to(device=dev, dtype=torch.float32).contiguous()
+        hb32 = hb.to(device=dev, dtype=torch.float32).contiguous() if hb is not None else None
+        out = torch.zeros(N, hc, oh, ow, dtype=torch.float32, device=dev)
+        L.check(L.lib().dbsr_conv2d_head(d, hw32.data_ptr(), hb32.data_ptr() if hb32 is not None else None, hc,
+                                         L.tensor_desc(out, 1, 0, img_stride=hc * oh * ow, dtype=torch.float32),
+                                         s), 'dbsr_conv2d_head')
+        return out
     L.check(L.lib().dbsr_conv2d(d, s), 'dbsr_conv2d')
     return y[..., :Cout].permute(0, 3, 1, 2).contiguous()

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define DBSR_ABI_VERSION 2
+#define DBSR_ABI_VERSION 3
 
 enum { DBSR_F32 = 0, DBSR_BF16 = 1 };
 enum { DBSR_ACT_NONE = 0, DBSR_ACT_RELU = 1, DBSR_ACT_LRELU = 2 };      /* LeakyReLU slope 0.1 */
@@ -107,6 +107,16 @@ int dbsr_set_conv_algo(int algo);
 /* Which kernel dbsr_conv2d would launch for `d` under the current selection: 2 pipelined, 1 LDS-tiled,
  * 0 generic. */
 int dbsr_conv_kernel_for(const dbsr_conv_desc* d);
+/* A 32-channel ResBlock conv2 fused with a 1x1 head (the decoder's last post-ResBlock + RGB predictor,
+ * decoders.py:59-61 / blocks.py:94-96): t = ReLU(conv(x) + bias + residual) stays in registers (d->y is
+ * not written) and out = ReLU(head_w . t + head_b) is stored fp32 NCHW (head_out.img_stride =
+ * head_cout*out_h*out_w).  head_w: fp32 [head_cout][32] (the torch [head_cout][32][1][1] weight),
+ * head_b: fp32 [head_cout] or NULL, head_cout 1..4.  Requires dbsr_conv_head_ok(d). */
+int dbsr_conv2d_head(const dbsr_conv_desc* d, const float* head_w, const float* head_b, int head_cout,
+                     dbsr_tensor head_out, void* stream);
+/* 1 when dbsr_conv2d_head accepts `d`: pipelined shape (bf16 3x3/s1/p1, width % 64 == 0, height % 8 == 0,
+ * >= 256 tiles), cout == 32, residual, act none, post-act ReLU. */
+int dbsr_conv_head_ok(const dbsr_conv_desc* d);
 /* Scratch bytes dbsr_conv2d would use for split-K on `d` (0 = no split).  Convs whose grid cannot fill
  * the chip split K into slices that store fp32 partials to `workspace`; a second launch sums them in
  * slice order (deterministic) and applies the epilogue.  With a smaller/NULL workspace the conv simply

@@ -196,3 +196,38 @@ def test_conv2d_pipelined(ops, case):
     np.testing.assert_allclose(outs[3].numpy(), outs[1].numpy(), atol=3e-2, rtol=2e-2)
     np.testing.assert_allclose(outs[3].numpy(), outs[0].numpy(), atol=3e-2, rtol=2e-2)
     assert (outs[3] - ref).abs().mean() < 3e-3
+
+
+@pytest.mark.parametrize('case', [(2, 32, 16, 128, 3), (1, 32, 24, 64, 1), (3, 32, 8, 192, 4)])
+def test_conv2d_fused_head(ops, case):
+    """Last decoder ResBlock conv2 + RGB predictor in one pipelined kernel (dbsr_conv2d_head) against
+    torch fp32 on the same bf16-rounded operands: relu(W_h . relu(conv(x) + b + res) + b_h)."""
+    from dbsr_amd import _lib
+    N, C, H, W, hc = case
+    gen = torch.Generator().manual_seed(H * 31 + W + hc)
+    x = torch.randn(N, C, H, W, generator=gen)
+    w = torch.randn(C, C, 3, 3, generator=gen) / (C * 9) ** 0.5
+    b = torch.randn(C, generator=gen) * 0.1
+    res = torch.randn(N, C, H, W, generator=gen)
+    hw = torch.randn(hc, C, 1, 1, generator=gen) / C ** 0.5
+    hb = torch.randn(hc, generator=gen) * 0.1
+    xb, wb, rb = (t.to(torch.bfloat16).float() for t in (x, w, res))
+    ref = F.relu(F.conv2d(F.relu(F.conv2d(xb, wb, b, padding=1) + rb), hw, hb))
+    try:
+        _lib.lib().dbsr_set_conv_algo(3)      # pipelined kernel at any tile count
+        out = ops.conv2d(x.to(DEV), w.to(DEV), b.to(DEV), padding=1, act=0, residual=res.to(DEV), post_act=1,
+                         compute_dtype=torch.bfloat16, head=(hw.to(DEV), hb.to(DEV))).cpu()
+    finally:
+        _lib.lib().dbsr_set_conv_algo(2)
+    assert out.shape == (N, hc, H, W)
+    # fp32 head on the fp32 ResBlock output: only the bf16 operands of the 3x3 conv differ from torch
+    np.testing.assert_allclose(out.numpy(), ref.numpy(), atol=2e-3, rtol=2e-3)
+
+
+def test_conv2d_head_rejects_ineligible(ops):
+    """A conv the fused head cannot serve (64 couts) is refused with an error, never silently run."""
+    x = torch.randn(1, 64, 8, 64, device=DEV)
+    w = torch.randn(64, 64, 3, 3, device=DEV)
+    with pytest.raises(RuntimeError, match='conv2d_head'):
+        ops.conv2d(x, w, None, padding=1, residual=torch.randn(1, 64, 8, 64, device=DEV), post_act=1,
+                   compute_dtype=torch.bfloat16, head=(torch.randn(3, 64, 1, 1, device=DEV), None))
