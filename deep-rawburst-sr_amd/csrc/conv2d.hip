@@ -1139,6 +1139,116 @@ int dispatch_conv(const ConvK& k, const dbsr_conv_desc* d, hipStream_t s) {
     return launch_conv<T, 1, 1>(kk, s);
 }
 
+// ------------------------------------------------------------------------------------------------
+// PixelShuffle upsampler (upsampling.py:51-66; decoders.py:43): 1x1 conv Cin -> s*s*32 (+ bias, act),
+// written as PixelShuffle(s) of the result.  bf16, Cin padded to a multiple of 32 (<= 128), 32 output
+// channels per sub-pixel, s*s % 8 == 0.
+// Block = 8 waves over PG*16 consecutive low-res pixels; wave w owns sub-pixels w, w+8, ... (for s = 8
+// the column sx = w of every sub-pixel row).  The pixels' K values are loaded once (PG*KS B-fragments);
+// per sub-pixel the wave runs 2 x PG x KS MFMAs against that sub-pixel's 32 weight rows (prefetched
+// one sub-pixel ahead), read in the order c = 8(m>>2) + 4h + (m&3) for MFMA row m of half h, so lane
+// (g, col) ends up with channels 8g..8g+7 of its pixel: one 16-B store per lane, 64 contiguous bytes
+// (the whole 32-channel output pixel) per 4 lanes.
+// ------------------------------------------------------------------------------------------------
+template <int PG, int KS>
+__global__ __launch_bounds__(512) void upsample_shuffle_kernel(ConvK k) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int g = lane >> 4, col = lane & 15;
+    const int s = k.shuffle, s2 = s * s;
+    const int hw = k.out_h * k.out_w;
+    Frag<bf16_t> b[PG][KS];
+    int pf[PG], py[PG], px[PG];
+#pragma unroll
+    for (int j = 0; j < PG; ++j) {
+        const int p = blockIdx.x * (PG * 16) + j * 16 + col;
+        const bool ok = p < k.npix;
+        const int f = ok ? p / hw : 0, rr = ok ? p - f * hw : 0;
+        pf[j] = ok ? f : -1;
+        py[j] = rr / k.out_w;
+        px[j] = rr - py[j] * k.out_w;
+        const bf16_t* xp = (const bf16_t*)k.x + map_frame(k.xm, f) * k.x_is + (long long)rr * k.x_ld + g * 8;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            if (ok) b[j][ks].load(xp + ks * 32);
+            else b[j][ks].zero();
+        }
+    }
+    const int m_row = 8 * (col >> 2) + (col & 3);           // + 4h: packed row within the sub-pixel's 32
+    auto load_a = [&](int sub, Frag<bf16_t> (&a)[2][KS]) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks)
+                a[h][ks].load((const bf16_t*)k.w + (long long)(sub * 32 + m_row + 4 * h) * k.Kp + ks * 32 + g * 8);
+    };
+    Frag<bf16_t> a_cur[2][KS], a_nxt[2][KS];
+    int sub = wave;
+    if (sub < s2) load_a(sub, a_cur);
+    for (; sub < s2; sub += 8) {
+        if (sub + 8 < s2) load_a(sub + 8, a_nxt);
+        f32x4_t acc[2][PG];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int j = 0; j < PG; ++j) {
+                acc[h][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks) acc[h][j] = mma(a_cur[h][ks], b[j][ks], acc[h][j]);
+            }
+        const float* bp = k.bias + sub * 32 + 8 * g;
+        float bv[8];
+        if (k.bias) {
+            const float4 b0 = *(const float4*)bp, b1 = *(const float4*)(bp + 4);
+            bv[0] = b0.x; bv[1] = b0.y; bv[2] = b0.z; bv[3] = b0.w; bv[4] = b1.x; bv[5] = b1.y; bv[6] = b1.z; bv[7] = b1.w;
+        } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) bv[e] = 0.f;
+        }
+        const int sy = sub / s, sx = sub - sy * s;
+#pragma unroll
+        for (int j = 0; j < PG; ++j) {
+            if (pf[j] < 0) continue;
+            u32x4_t o;
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                o[e] = pack_bf16x2(apply_act(acc[0][j][2 * e] + bv[2 * e], k.act),
+                                   apply_act(acc[0][j][2 * e + 1] + bv[2 * e + 1], k.act));
+                o[2 + e] = pack_bf16x2(apply_act(acc[1][j][2 * e] + bv[4 + 2 * e], k.act),
+                                       apply_act(acc[1][j][2 * e + 1] + bv[4 + 2 * e + 1], k.act));
+            }
+            const long long Y = (long long)py[j] * s + sy, X = (long long)px[j] * s + sx;
+            *(u32x4_t*)((bf16_t*)k.y + map_frame(k.ym, pf[j]) * k.y_is + (Y * (k.out_w * s) + X) * k.y_ld + k.y_c0 +
+                        8 * g) = o;
+        }
+        if (sub + 8 < s2) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks) a_cur[h][ks] = a_nxt[h][ks];
+        }
+    }
+}
+
+bool use_upsample(const dbsr_conv_desc* d, const ConvK& k) {
+    return d->x.dtype == DBSR_BF16 && d->y.dtype == DBSR_BF16 && !d->precise && d->out_mode == DBSR_OUT_SHUFFLE &&
+           d->kh == 1 && d->kw == 1 && d->stride == 1 && d->pad == 0 && k.cps == 32 &&
+           (d->shuffle * d->shuffle) % 8 == 0 && k.Kp % 32 == 0 && k.Kp <= 128 && d->y.ld % 8 == 0 &&
+           d->y.c0 % 8 == 0 && g_tiled_enabled;
+}
+
+int launch_upsample(const ConvK& k, hipStream_t s) {
+    const int pg = (k.npix + 63) / 64 >= 512 ? 4 : 2;
+    const unsigned grid = (unsigned)((k.npix + pg * 16 - 1) / (pg * 16));
+    const int ks = k.Kp / 32;
+#define DBSR_UP(PG, KS) \
+    if (pg == PG && ks == KS) hipLaunchKernelGGL((upsample_shuffle_kernel<PG, KS>), dim3(grid), dim3(512), 0, s, k)
+    DBSR_UP(2, 1); DBSR_UP(2, 2); DBSR_UP(2, 3); DBSR_UP(2, 4);
+    DBSR_UP(4, 1); DBSR_UP(4, 2); DBSR_UP(4, 3); DBSR_UP(4, 4);
+#undef DBSR_UP
+    DBSR_LAUNCH_CHECK();
+    return 0;
+}
+
 ConvK make_convk(const dbsr_conv_desc* d) {
     ConvK k;
     k.x = d->x.ptr; k.x_is = d->x.img_stride; k.x_ld = d->x.ld; k.xm = d->x.map; k.in_h = d->in_h; k.in_w = d->in_w;
@@ -1170,6 +1280,7 @@ ConvK make_convk(const dbsr_conv_desc* d) {
 extern "C" int dbsr_conv_kernel_for(const dbsr_conv_desc* d) {
     if (!d) return -1;
     if (pick_pipe(d)) return 2;
+    if (use_upsample(d, make_convk(d))) return 3;
     return use_tiled(d) ? 1 : 0;
 }
 
@@ -1179,7 +1290,7 @@ extern "C" int dbsr_conv_head_ok(const dbsr_conv_desc* d) {
 }
 
 extern "C" size_t dbsr_conv_workspace_bytes(const dbsr_conv_desc* d) {
-    if (!d || pick_pipe(d) || use_tiled(d) || d->precise) return 0;
+    if (!d || pick_pipe(d) || use_tiled(d) || d->precise || use_upsample(d, make_convk(d))) return 0;
     const ConvK k = make_convk(d);
     int m, n;
     pick_generic_tile(k, m, n);
@@ -1263,6 +1374,7 @@ extern "C" int dbsr_conv2d(const dbsr_conv_desc* d, void* stream) {
         if (k.npix >= 512 * 128) return launch_conv<float, 1, 2, bf16_t>(k, s);
         return launch_conv<float, 1, 1, bf16_t>(k, s);
     }
+    if (use_upsample(d, k)) return launch_upsample(k, s);
     return d->x.dtype == DBSR_BF16 ? dispatch_conv<bf16_t>(k, d, s) : dispatch_conv<float>(k, d, s);
 }
 

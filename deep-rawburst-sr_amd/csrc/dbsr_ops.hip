@@ -290,32 +290,58 @@ __global__ void merge_prep_kernel(int B, int N, int hw, int C, dbsr_tensor proj,
 struct K9 {
     float k[9];
 };
+// Thread = (frame, 8-channel group, column, strip of BLUR_ROWS rows): it slides a 3-row window down
+// its strip, loading each input row's 3 column neighbours once (3 16-B loads per output instead of 9);
+// consecutive threads are consecutive (group, column), so every row load is a coalesced 16-B-per-lane
+// sweep of one image row.
+constexpr int BLUR_ROWS = 8;
 template <typename T>
-__global__ void blur3_kernel(int n, int h, int w, int groups, dbsr_tensor in, K9 kk, dbsr_tensor out) {
+__global__ __launch_bounds__(256) void blur3_kernel(int n, int h, int w, int groups, dbsr_tensor in, K9 kk,
+                                                    dbsr_tensor out) {
     const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= (long long)n * h * w * groups) return;
+    const int strips = (h + BLUR_ROWS - 1) / BLUR_ROWS;
+    if (idx >= (long long)n * strips * w * groups) return;
     const int g = (int)(idx % groups);
-    const long long pix = idx / groups;
-    const int f = (int)(pix / (h * w)), rr = (int)(pix - (long long)f * h * w);
-    const int y = rr / w, x = rr - y * w;
+    long long r = idx / groups;
+    const int x = (int)(r % w);
+    r /= w;
+    const int st = (int)(r % strips);
+    const int f = (int)(r / strips);
     const T* base = img_ptr<T>(in, f) + g * 8;
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        const int yy = y + i - 1;
-        if ((unsigned)yy >= (unsigned)h) continue;
+    T* obase = img_ptr<T>(out, f) + g * 8;
+    float win[3][3][8];                       // [row slot][column -1..+1][channel]
+    auto load_row = [&](int yy, float (&dst)[3][8]) {
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
             const int xx = x + j - 1;
-            if ((unsigned)xx >= (unsigned)w) continue;
-            float v[8];
-            load8(base + ((long long)yy * w + xx) * in.ld, v);
-            const float kv = kk.k[i * 3 + j];
+            if ((unsigned)yy < (unsigned)h && (unsigned)xx < (unsigned)w) {
+                load8(base + ((long long)yy * w + xx) * in.ld, dst[j]);
+            } else {
 #pragma unroll
-            for (int q = 0; q < 8; ++q) acc[q] = fmaf(kv, v[q], acc[q]);
+                for (int q = 0; q < 8; ++q) dst[j][q] = 0.f;
+            }
         }
+    };
+    const int y0 = st * BLUR_ROWS;
+    load_row(y0 - 1, win[0]);
+    load_row(y0, win[1]);
+#pragma unroll
+    for (int t = 0; t < BLUR_ROWS; ++t) {
+        const int y = y0 + t;
+        if (y >= h) break;
+        // rotating slots: rows y-1, y, y+1 sit in slots t%3, (t+1)%3, (t+2)%3 (unrolled: static indices)
+        load_row(y + 1, win[(t + 2) % 3]);
+        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const float kv = kk.k[i * 3 + j];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) acc[q] = fmaf(kv, win[(t + i) % 3][j][q], acc[q]);
+            }
+        store8(obase + ((long long)y * w + x) * out.ld, acc);
     }
-    store8(img_ptr<T>(out, f) + (long long)rr * out.ld + g * 8, acc);
 }
 
 inline unsigned nblocks(long long total, int bs) { return (unsigned)((total + bs - 1) / bs); }
@@ -412,7 +438,7 @@ extern "C" int dbsr_gauss_blur3(int n, int h, int w, int c, dbsr_tensor in, cons
     DBSR_CHECK_ARG(c % 8 == 0 && vec_ok(in, 8) && vec_ok(out, 8), "blur: layout");
     K9 kk;
     for (int i = 0; i < 9; ++i) kk.k[i] = k_host[i];
-    const long long total = (long long)n * h * w * (c / 8);
+    const long long total = (long long)n * ((h + BLUR_ROWS - 1) / BLUR_ROWS) * w * (c / 8);
     return by_dtype(in.dtype, [&](auto* tag) {
         using T = std::remove_pointer_t<decltype(tag)>;
         hipLaunchKernelGGL(blur3_kernel<T>, dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, n, h, w,

@@ -79,10 +79,11 @@ def warp(feat, flow, mode='bilinear', padding_mode='zeros'):
 
 
 def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, act=L.ACT_NONE, residual=None,
-           post_act=L.ACT_NONE, compute_dtype=torch.float32, out_f32=False, head=None):
+           post_act=L.ACT_NONE, compute_dtype=torch.float32, out_f32=False, head=None, shuffle=1):
     """act(conv2d(x) + bias) (+ residual, then post_act); NCHW in/out, computed by dbsr_conv2d.
     head = (w [hc, Cout, 1, 1], b [hc] | None): return ReLU(conv1x1(result, w, b)) as fp32 NCHW instead,
-    computed by dbsr_conv2d_head (the conv's own result is not stored)."""
+    computed by dbsr_conv2d_head (the conv's own result is not stored).
+    shuffle = s > 1: return PixelShuffle(s) of the result (upsampling.py:51-66's conv + shuffle)."""
     _need_cuda(x, weight)
     N, Cin, H, W = x.shape
     Cout, _, kh, kw = weight.shape
@@ -95,13 +96,14 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, act=L.ACT_NONE
     b32 = bias.to(torch.float32).contiguous() if bias is not None else None
     s = L.stream_ptr(dev)
     L.check(L.lib().dbsr_conv_pack_weights(w32.data_ptr(), b32.data_ptr() if b32 is not None else None, Cout, Cin,
-                                           kh, kw, L.dtype_code(compute_dtype), 1, wp.data_ptr(),
+                                           kh, kw, L.dtype_code(compute_dtype), shuffle, wp.data_ptr(),
                                            bp.data_ptr() if bp is not None else None, s), 'pack')
     oh = (H + 2 * padding - dilation * (kh - 1) - 1) // stride + 1
     ow = (W + 2 * padding - dilation * (kw - 1) - 1) // stride + 1
     ody = torch.float32 if out_f32 else compute_dtype
-    ldy = (Cout + 7) // 8 * 8
-    y = torch.zeros(N, oh, ow, ldy, dtype=ody, device=dev)
+    pc = Cout // (shuffle * shuffle)
+    ldy = (pc + 7) // 8 * 8
+    y = torch.zeros(N, oh * shuffle, ow * shuffle, ldy, dtype=ody, device=dev)
     d = L.ConvDesc()
     d.n_frames = N
     d.x = L.tensor_desc(xs, ldx)
@@ -118,7 +120,7 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, act=L.ACT_NONE
     else:
         d.res = L.NULL_TENSOR
     d.post_act = post_act
-    d.out_mode, d.shuffle = L.OUT_NHWC, 0
+    d.out_mode, d.shuffle = (L.OUT_SHUFFLE, shuffle) if shuffle > 1 else (L.OUT_NHWC, 0)
     need = L.lib().dbsr_conv_workspace_bytes(d)
     ws = torch.zeros(max(need // 4, 1), dtype=torch.float32, device=dev)
     d.workspace, d.workspace_bytes = ws.data_ptr(), need
@@ -133,4 +135,4 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, act=L.ACT_NONE
                                          s), 'dbsr_conv2d_head')
         return out
     L.check(L.lib().dbsr_conv2d(d, s), 'dbsr_conv2d')
-    return y[..., :Cout].permute(0, 3, 1, 2).contiguous()
+    return y[..., :pc].permute(0, 3, 1, 2).contiguous()

@@ -231,3 +231,47 @@ def test_conv2d_head_rejects_ineligible(ops):
     with pytest.raises(RuntimeError, match='conv2d_head'):
         ops.conv2d(x, w, None, padding=1, residual=torch.randn(1, 64, 8, 64, device=DEV), post_act=1,
                    compute_dtype=torch.bfloat16, head=(torch.randn(3, 64, 1, 1, device=DEV), None))
+
+
+@pytest.mark.parametrize('case', [(2, 64, 6, 10, 8), (1, 64, 48, 48, 8), (3, 32, 5, 7, 4), (1, 128, 4, 9, 8)])
+def test_conv1x1_pixelshuffle(ops, case):
+    """PixelShuffle upsampler (1x1 conv + ReLU + shuffle, upsampling.py:51-66): the dedicated bf16 kernel
+    (dbsr_conv_kernel_for == 3) against torch on the same bf16-rounded operands and against the generic
+    kernel's shuffle epilogue (algo 0)."""
+    from dbsr_amd import _lib
+    N, Cin, H, W, s = case
+    Cout = 32 * s * s
+    gen = torch.Generator().manual_seed(Cin + H * W + s)
+    x = torch.randn(N, Cin, H, W, generator=gen)
+    w = torch.randn(Cout, Cin, 1, 1, generator=gen) / Cin ** 0.5
+    b = torch.randn(Cout, generator=gen) * 0.1
+    xb, wb = x.to(torch.bfloat16).float(), w.to(torch.bfloat16).float()
+    ref = F.pixel_shuffle(F.relu(F.conv2d(xb, wb, b)), s)
+    outs = {}
+    try:
+        for algo in (2, 0):
+            _lib.lib().dbsr_set_conv_algo(algo)
+            outs[algo] = ops.conv2d(x.to(DEV), w.to(DEV), b.to(DEV), act=1, compute_dtype=torch.bfloat16,
+                                    shuffle=s).float().cpu()
+    finally:
+        _lib.lib().dbsr_set_conv_algo(2)
+    assert outs[2].shape == ref.shape
+    np.testing.assert_allclose(outs[2].numpy(), ref.numpy(), atol=2e-2, rtol=1e-2)
+    np.testing.assert_array_equal(outs[2].numpy(), outs[0].numpy())
+
+
+@pytest.mark.parametrize('shape', [(2, 32, 384, 384), (1, 16, 13, 21), (3, 8, 9, 4)])
+def test_gauss_blur3(shape):
+    """Sliding-window 3x3 Gaussian (upsampling.py:59-65, filtering.py:29-40) against the oracle's blur."""
+    from dbsr_amd import _lib as L
+    N, C, H, W = shape
+    x = torch.randn(N, C, H, W, generator=torch.Generator().manual_seed(H + W + C))
+    kern = orc.gauss_kernel(3, 1.0).reshape(3, 3).float()
+    ref = F.conv2d(x, kern.expand(C, 1, 3, 3).contiguous(), padding=1, groups=C)
+    xs = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+    out = torch.zeros_like(xs)
+    import ctypes
+    kb = (ctypes.c_float * 9)(*kern.flatten().tolist())
+    L.check(L.lib().dbsr_gauss_blur3(N, H, W, C, L.tensor_desc(xs, C), kb, L.tensor_desc(out, C),
+                                     L.stream_ptr(xs.device)), 'blur')
+    np.testing.assert_allclose(out.permute(0, 3, 1, 2).cpu().numpy(), ref.numpy(), atol=1e-5, rtol=1e-5)
