@@ -70,3 +70,41 @@ def test_graph_replay_matches_eager(golden, synth_sd):
         p2, _ = net(burst * 0.5)
     assert torch.equal(p0, p1) and torch.equal(a0['offsets'], o1)
     assert not torch.equal(p1, p2)
+
+
+def test_cfg3_burstsr_shape_fp32(synth_sd):
+    """configs[2] shape (BurstSR real crops: 14 frames, 80x80, fp32) against the oracle on the same
+    input.  Real-RAW layout: black-level-subtracted 10-bit values /1023 (burstsr_dataset.py:57,78-90),
+    emulated by quantising a synthetic burst to 1/1023 steps.  80 is not a multiple of 64, so PWC-Net's
+    resize-to-128 path (pwcnet.py:256-259) and the W/W64 flow rescale are exercised."""
+    from dbsr_amd.burst import synthetic_bursts
+    from oracle import dbsr_oracle as orc
+    burst, _ = synthetic_bursts(1, 14, 80, 80, sr_factor=8, seed=11)
+    burst = (burst * 1023).round() / 1023
+    net = _net(synth_sd, torch.float32)
+    with torch.no_grad():
+        pred, aux = net(burst.to(DEV))
+    ref, raux = orc.dbsr_forward(burst, synth_sd)
+    assert pred.shape == (1, 3, 640, 640)
+    assert (aux['offsets'].cpu() - raux['offsets']).abs().max().item() <= 1e-3
+    assert (pred.cpu() - ref).abs().max().item() <= 1e-3
+
+
+def test_compute_score_hip_vs_oracle(tmp_path, synth_sd):
+    """SyntheticBurstVal-layout files -> evaluation.compute_score with the HIP bf16 network (batched)
+    vs the same scoring of the oracle's fp32 forward, per image within the 0.01 dB bar."""
+    from dbsr_amd import evaluation as ev
+    from dbsr_amd.burst import synthetic_bursts
+    from oracle import dbsr_oracle as orc
+    burst, gt = synthetic_bursts(2, 14, 48, 48, sr_factor=8, seed=21)
+    ev.write_synthetic_burst_val(str(tmp_path), burst, gt)
+    ds = ev.SyntheticBurstVal(str(tmp_path))
+    net = _net(synth_sd, torch.bfloat16)
+    mine = ev.compute_score(net, ds, boundary_ignore=40, device=DEV, batch=2)
+    psnr = ev.PSNR(boundary_ignore=40)
+    for i in range(len(ds)):
+        b, g, meta = ds[i]
+        ref, _ = orc.dbsr_forward(b.unsqueeze(0), synth_sd)
+        r = float(psnr(ev.quantize_prediction(ref), g.unsqueeze(0)))
+        print(meta['burst_name'], mine['per_image'][meta['burst_name']], r)
+        assert abs(mine['per_image'][meta['burst_name']] - r) <= 0.01
