@@ -1,5 +1,7 @@
 // DBSR merge-path kernels: flow-guided warp of the frame embeddings (HBM-bound), softmax-over-burst
 // fusion (HBM-bound), merge input prep and the decoder's Gaussian blur.  NHWC activations.
+#include <cstdlib>
+#include <type_traits>
 #include "common.hpp"
 
 using namespace dbsr;
@@ -262,6 +264,88 @@ __global__ __launch_bounds__(256) void fuse_softmax_kernel(int B, int N, int hw,
     Vec4<T>::st(img_ptr<T>(fused, b) + (long long)rr * fused.ld + c, acc);
 }
 
+// bf16, C == 512: one wave per pixel, 8 channels per lane, so every logit/feature/weight access is a
+// 16-B-per-lane sweep of one 1-KiB pixel row (the 4-channel kernel above moves 8 B per lane and needs
+// twice the memory instructions).  All 2N loads are issued before the first use; the logits are
+// consumed once, so they are streamed with non-temporal loads, and the aux weights (written once,
+// never re-read by the forward) with non-temporal stores, keeping L2 for the feature rows.
+template <int NMAX>
+__global__ __launch_bounds__(256) void fuse512_bf16_kernel(int B, int N, int hw, dbsr_tensor logits, dbsr_tensor ref,
+                                                           dbsr_tensor oth, dbsr_tensor fused, dbsr_tensor weights) {
+    const unsigned pix = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    if (pix >= (unsigned)B * hw) return;
+    const int b = (int)(pix / hw), rr = (int)(pix - (unsigned)b * hw);
+    const int c = (threadIdx.x & 63) * 8;
+    u32x4_t lr[NMAX], fr[NMAX];
+#pragma unroll
+    for (int n = 0; n < NMAX; ++n) {
+        if (n < N) {
+            lr[n] = __builtin_nontemporal_load(
+                (const u32x4_t*)(img_ptr<bf16_t>(logits, b * N + n) + (long long)rr * logits.ld + c));
+            const bf16_t* fp = n == 0 ? img_ptr<bf16_t>(ref, b) + (long long)rr * ref.ld
+                                      : img_ptr<bf16_t>(oth, b * (N - 1) + n - 1) + (long long)rr * oth.ld;
+            fr[n] = *(const u32x4_t*)(fp + c);
+        }
+    }
+    float m[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m[j] = -INFINITY;
+#pragma unroll
+    for (int n = 0; n < NMAX; ++n) {
+        if (n < N) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                m[2 * j] = fmaxf(m[2 * j], __uint_as_float(lr[n][j] << 16));
+                m[2 * j + 1] = fmaxf(m[2 * j + 1], __uint_as_float(lr[n][j] & 0xffff0000u));
+            }
+        }
+    }
+    float e[NMAX][8], s[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] = 0.f;
+#pragma unroll
+    for (int n = 0; n < NMAX; ++n) {
+        if (n < N) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                e[n][2 * j] = __expf(__uint_as_float(lr[n][j] << 16) - m[2 * j]);
+                e[n][2 * j + 1] = __expf(__uint_as_float(lr[n][j] & 0xffff0000u) - m[2 * j + 1]);
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) s[j] += e[n][j];
+        }
+    }
+    float inv[8], acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        inv[j] = 1.0f / s[j];
+        acc[j] = 0.f;
+    }
+#pragma unroll
+    for (int n = 0; n < NMAX; ++n) {
+        if (n < N) {
+            float wn[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) wn[j] = e[n][j] * inv[j];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                acc[2 * j] = fmaf(__uint_as_float(fr[n][j] << 16), wn[2 * j], acc[2 * j]);
+                acc[2 * j + 1] = fmaf(__uint_as_float(fr[n][j] & 0xffff0000u), wn[2 * j + 1], acc[2 * j + 1]);
+            }
+            if (weights.ptr) {
+                u32x4_t o;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(wn[2 * j], wn[2 * j + 1]);
+                __builtin_nontemporal_store(o, (u32x4_t*)(img_ptr<bf16_t>(weights, b * N + n) + (long long)rr * weights.ld + c));
+            }
+        }
+    }
+    u32x4_t o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(acc[2 * j], acc[2 * j + 1]);
+    *(u32x4_t*)(img_ptr<bf16_t>(fused, b) + (long long)rr * fused.ld + c) = o;
+}
+
 // ------------------------------------------------------------------------------------------------
 // merge prep (merging.py:79-89): out = [proj[b,0] | proj[b,n] - proj[b,0]]
 // ------------------------------------------------------------------------------------------------
@@ -383,6 +467,15 @@ extern "C" int dbsr_warp_bilinear(int n, int h, int w, int c, dbsr_tensor feat, 
     });
 }
 
+// DBSR_FUSE512=0 selects the 4-channel kernel for A/B runs (default: the 512-channel bf16 kernel)
+static bool fuse512_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("DBSR_FUSE512");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 extern "C" int dbsr_fuse_softmax(int B, int N, int hw, int c, dbsr_tensor logits, dbsr_tensor ref, dbsr_tensor oth,
                                  dbsr_tensor fused, dbsr_tensor weights, void* stream) {
     DBSR_CHECK_ARG(map_ok(logits) && map_ok(ref) && map_ok(fused) && (N == 1 || map_ok(oth)), "fuse: bad tensor");
@@ -397,6 +490,27 @@ extern "C" int dbsr_fuse_softmax(int B, int N, int hw, int c, dbsr_tensor logits
     return by_dtype(ref.dtype, [&](auto* tag) {
         using T = std::remove_pointer_t<decltype(tag)>;
         const bool wp = groups % 64 == 0;
+        if constexpr (std::is_same_v<T, bf16_t>) {
+            if (c == 512 && fuse512_enabled() && vec_ok(logits, 8) && vec_ok(ref, 8) && vec_ok(fused, 8) &&
+                (N == 1 || vec_ok(oth, 8)) && (!weights.ptr || (weights.dtype == DBSR_BF16 && vec_ok(weights, 8)))) {
+                const long long waves = (long long)B * hw;
+#define DBSR_FUSE512(NM)                                                                                       \
+    hipLaunchKernelGGL((fuse512_bf16_kernel<NM>), dim3(nblocks(waves, 4)), dim3(256), 0, (hipStream_t)stream, B, N, \
+                       hw, logits, ref, oth, fused, weights);
+                if (N <= 4) {
+                    DBSR_FUSE512(4)
+                } else if (N <= 8) {
+                    DBSR_FUSE512(8)
+                } else if (N == 14) {
+                    DBSR_FUSE512(14)
+                } else {
+                    DBSR_FUSE512(16)
+                }
+#undef DBSR_FUSE512
+                DBSR_LAUNCH_CHECK();
+                return 0;
+            }
+        }
 #define DBSR_FUSE(NM)                                                                                         \
     if (wp)                                                                                                   \
         hipLaunchKernelGGL((fuse_softmax_kernel<T, NM, true>), dim3(nblocks(total, 256)), dim3(256), 0,       \
