@@ -347,6 +347,93 @@ __global__ __launch_bounds__(256) void fuse512_bf16_kernel(int B, int N, int hw,
 }
 
 // ------------------------------------------------------------------------------------------------
+// Frame-sharded fusion (SURVEY §8e, configs[4]): the softmax over the burst (merging.py:116-124)
+// split over ranks that each hold a subset of the frames.  Rank-local partial statistics per
+// (b, pixel, channel): m = max_n l_n, s = sum_n exp(l_n - m), a = sum_n exp(l_n - m) * f_n over the
+// local frames [first, N); then a log-sum-exp combine over the R ranks' statistics:
+// fused = (sum_r a_r e^(m_r - M)) / (sum_r s_r e^(m_r - M)), M = max_r m_r.  Same value as
+// sum_n f_n softmax(l)_n up to fp32 rounding order.  stats: fp32 [B][hw][3c] = (m | s | a).
+// ------------------------------------------------------------------------------------------------
+template <typename T, int NMAX>
+__global__ __launch_bounds__(256) void fuse_partial_kernel(int B, int N, int hw, int groups, int first,
+                                                           dbsr_tensor logits, dbsr_tensor ref, dbsr_tensor oth,
+                                                           float* __restrict__ stats) {
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long long)B * hw * groups) return;
+    const int g = (int)(idx % groups);
+    const long long pix = idx / groups;
+    const int b = (int)(pix / hw), rr = (int)(pix - (long long)b * hw);
+    const int c = g * 4, C = groups * 4;
+    float l[NMAX][4];
+    float m[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY}, s[4] = {0.f, 0.f, 0.f, 0.f}, a[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int n = 0; n < NMAX; ++n) {
+        if (n >= first && n < N) {
+            Vec4<T>::ld(img_ptr<T>(logits, b * N + n) + (long long)rr * logits.ld + c, l[n]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) m[j] = fmaxf(m[j], l[n][j]);
+        }
+    }
+#pragma unroll
+    for (int n = 0; n < NMAX; ++n) {
+        if (n >= first && n < N) {
+            float fv[4];
+            const T* fp = n == 0 ? img_ptr<T>(ref, b) + (long long)rr * ref.ld
+                                 : img_ptr<T>(oth, b * (N - 1) + n - 1) + (long long)rr * oth.ld;
+            Vec4<T>::ld(fp + c, fv);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float e = __expf(l[n][j] - m[j]);
+                s[j] += e;
+                a[j] = fmaf(fv[j], e, a[j]);
+            }
+        }
+    }
+    float* o = stats + pix * 3 * C + c;
+    Vec4<float>::st(o, m);
+    Vec4<float>::st(o + C, s);
+    Vec4<float>::st(o + 2 * C, a);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void fuse_combine_kernel(int R, int B, int hw, int groups,
+                                                           const float* __restrict__ stats, dbsr_tensor fused) {
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long total = (long long)B * hw * groups;
+    if (idx >= total) return;
+    const int g = (int)(idx % groups);
+    const long long pix = idx / groups;
+    const int b = (int)(pix / hw), rr = (int)(pix - (long long)b * hw);
+    const int c = g * 4, C = groups * 4;
+    const long long rank_stride = (long long)B * hw * 3 * C;
+    float M[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    for (int r = 0; r < R; ++r) {
+        float m[4];
+        Vec4<float>::ld(stats + r * rank_stride + pix * 3 * C + c, m);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) M[j] = fmaxf(M[j], m[j]);
+    }
+    float S[4] = {0.f, 0.f, 0.f, 0.f}, A[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < R; ++r) {
+        const float* p = stats + r * rank_stride + pix * 3 * C + c;
+        float m[4], sv[4], av[4];
+        Vec4<float>::ld(p, m);
+        Vec4<float>::ld(p + C, sv);
+        Vec4<float>::ld(p + 2 * C, av);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float k = m[j] == -INFINITY ? 0.f : __expf(m[j] - M[j]);   // a rank with no frames adds nothing
+            S[j] = fmaf(sv[j], k, S[j]);
+            A[j] = fmaf(av[j], k, A[j]);
+        }
+    }
+    float out[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) out[j] = A[j] / S[j];
+    Vec4<T>::st(img_ptr<T>(fused, b) + (long long)rr * fused.ld + c, out);
+}
+
+// ------------------------------------------------------------------------------------------------
 // merge prep (merging.py:79-89): out = [proj[b,0] | proj[b,n] - proj[b,0]]
 // ------------------------------------------------------------------------------------------------
 template <typename T>
@@ -528,6 +615,42 @@ extern "C" int dbsr_fuse_softmax(int B, int N, int hw, int c, dbsr_tensor logits
             DBSR_FUSE(16)
         }
 #undef DBSR_FUSE
+        DBSR_LAUNCH_CHECK();
+        return 0;
+    });
+}
+
+extern "C" int dbsr_fuse_partial(int B, int N, int hw, int c, int first_frame, dbsr_tensor logits, dbsr_tensor ref,
+                                 dbsr_tensor oth, float* stats, void* stream) {
+    DBSR_CHECK_ARG(stats && map_ok(logits) && map_ok(ref) && (N == 1 || map_ok(oth)), "fuse_partial: bad tensor");
+    DBSR_CHECK_ARG(logits.dtype == ref.dtype && (N == 1 || oth.dtype == ref.dtype), "fuse_partial: dtype mismatch");
+    DBSR_CHECK_ARG(B > 0 && N > 0 && N <= 16 && hw > 0 && c % 4 == 0 && first_frame >= 0 && first_frame <= N,
+                   "fuse_partial: N in [1,16], c multiple of 4, first_frame in [0,N]");
+    DBSR_CHECK_ARG(vec_ok(logits, 4) && vec_ok(ref, 4) && (N == 1 || vec_ok(oth, 4)), "fuse_partial: ld/c0 % 4");
+    const int groups = c / 4;
+    const long long total = (long long)B * hw * groups;
+    return by_dtype(ref.dtype, [&](auto* tag) {
+        using T = std::remove_pointer_t<decltype(tag)>;
+        if (N <= 8)
+            hipLaunchKernelGGL((fuse_partial_kernel<T, 8>), dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream,
+                               B, N, hw, groups, first_frame, logits, ref, oth, stats);
+        else
+            hipLaunchKernelGGL((fuse_partial_kernel<T, 16>), dim3(nblocks(total, 256)), dim3(256), 0,
+                               (hipStream_t)stream, B, N, hw, groups, first_frame, logits, ref, oth, stats);
+        DBSR_LAUNCH_CHECK();
+        return 0;
+    });
+}
+
+extern "C" int dbsr_fuse_combine(int R, int B, int hw, int c, const float* stats, dbsr_tensor fused, void* stream) {
+    DBSR_CHECK_ARG(stats && map_ok(fused) && R > 0 && B > 0 && hw > 0 && c % 4 == 0 && vec_ok(fused, 4),
+                   "fuse_combine: bad arguments");
+    const int groups = c / 4;
+    const long long total = (long long)B * hw * groups;
+    return by_dtype(fused.dtype, [&](auto* tag) {
+        using T = std::remove_pointer_t<decltype(tag)>;
+        hipLaunchKernelGGL((fuse_combine_kernel<T>), dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, R,
+                           B, hw, groups, stats, fused);
         DBSR_LAUNCH_CHECK();
         return 0;
     });

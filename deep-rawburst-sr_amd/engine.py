@@ -475,7 +475,10 @@ class DBSREngine:
             a = c
         return (a, fused) if head is not None else a
 
-    def _build(self, B, N, H, W):
+    def _build(self, B, N, H, W, mode='full', first_frame=0):
+        """mode 'full': the whole forward.  mode 'partial' (frame-sharded fusion): stop after
+        the weight predictor and emit dbsr_fuse_partial statistics of frames [first_frame, N) into
+        bufs['stats'] instead of the fusion and the decoder (those run in `_build_combine`)."""
         dt, dev = self.dtype, self.device
         lib = L.lib()
         plan = Plan()
@@ -563,6 +566,16 @@ class DBSREngine:
         i = self._resblocks(plan, 'merge.wp.res', self.wp_res, F, hw, q, 0, dt)
         LG = NHWC(F, H, W, C, dt, dev)
         plan.conv('merge.wp.out', self.wp_out, F, q[i], 0, hw, LG, 0, L.ACT_NONE)
+        plan.keep.extend([raw, rgb, om, e, E, Wf, PJ, WP, o, q, LG])
+        if mode == 'partial':
+            ST = torch.zeros(B, H, W, 3 * C, dtype=torch.float32, device=dev)
+            plan.add('merge.fuse_partial', lib.dbsr_fuse_partial, B, N, H * W, C, first_frame, LG.d(0),
+                     E.d(0, (1, N, 0, 1)), Wf.d(0), ST.data_ptr())
+            bufs['stats'] = ST
+            plan.finalize_workspace(dev)
+            plan.bufs = bufs
+            plan.shape = (B, N, H, W)
+            return plan
         FUS = NHWC(B, H, W, C, dt, dev)
         FW = NHWC(F, H, W, C, dt, dev)
         bufs['fw_desc'] = FW.d(0)
@@ -570,7 +583,22 @@ class DBSREngine:
         plan.add('merge.fuse', lib.dbsr_fuse_softmax, *fuse_args)
         fuse_idx = len(plan.ops) - 1
         plan.fuse_bytes = ((2.0 * N + 1) * B * C * H * W * es, 1.0 * N * B * C * H * W * es)
-        # ---------------- decoder (decoders.py:54-62) ----------------
+        self._decoder(plan, B, H, W, FUS, bufs)
+        plan.keep.extend([FUS, FW])
+        plan.finalize_workspace(dev)
+        plan.bufs = bufs
+        plan.FW = FW
+        plan.fuse_idx = fuse_idx
+        plan.fuse_args = fuse_args
+        plan.shape = (B, N, H, W)
+        return plan
+
+    def _decoder(self, plan, B, H, W, FUS, bufs):
+        """ResPixShuffleConv (decoders.py:54-62) on the fused embedding FUS [B,H,W,C] -> bufs['pred']."""
+        dt, dev = self.dtype, self.device
+        lib = L.lib()
+        hw = (H, W)
+        S = self.s
         gd = self.dec_init.cout
         g = [NHWC(B, H, W, gd, dt, dev) for _ in range(3)]
         plan.conv('dec.init', self.dec_init, B, FUS, 0, hw, g[0], 0, L.ACT_RELU)
@@ -599,14 +627,7 @@ class DBSREngine:
         if not fused:
             plan.conv('dec.predictor', self.pred, B, sh[i], 0, (H * S, W * S), None, 0, L.ACT_RELU,
                       out_mode=L.OUT_NCHW_F32, y_desc=pdesc, precise=(dt == torch.bfloat16))
-        plan.keep.extend([raw, rgb, om, e, E, Wf, PJ, WP, o, q, LG, FUS, FW, g, sh])
-        plan.finalize_workspace(dev)
-        plan.bufs = bufs
-        plan.FW = FW
-        plan.fuse_idx = fuse_idx
-        plan.fuse_args = fuse_args
-        plan.shape = (B, N, H, W)
-        return plan
+        plan.keep.extend([g, sh])
 
     @staticmethod
     def _capture(plan, dev):
@@ -708,6 +729,67 @@ class DBSREngine:
         else:
             aux['fusion_weights'] = None
         return pred, aux
+
+
+    # ---------------- frame-sharded fusion (BASELINE configs[4]) ----------------
+    def _build_combine(self, R, B, H, W):
+        """dbsr_fuse_combine of R ranks' gathered statistics -> FUS, then the decoder."""
+        dt, dev = self.dtype, self.device
+        C = self.enc_out.cout
+        plan = Plan()
+        bufs = {'gathered': torch.zeros(R, B, H, W, 3 * C, dtype=torch.float32, device=dev)}
+        FUS = NHWC(B, H, W, C, dt, dev)
+        plan.add('merge.fuse_combine', L.lib().dbsr_fuse_combine, R, B, H * W, C, bufs['gathered'].data_ptr(),
+                 FUS.d(0))
+        self._decoder(plan, B, H, W, FUS, bufs)
+        plan.keep.append(FUS)
+        plan.finalize_workspace(dev)
+        plan.bufs = bufs
+        return plan
+
+    def _ready(self, burst):
+        if not burst.is_cuda:
+            raise RuntimeError('DBSRNet (MI355X engine) needs the burst on a HIP device; got %s' % burst.device)
+        if self.device != burst.device or self.sig != _param_signature(self.net):
+            self._pack(burst.device)
+
+    def forward_partial(self, burst, first_frame):
+        """Encoder, alignment, warp and weight predictor of a frame shard `burst` [B,n,4,H,W] (frame 0 =
+        the burst's reference frame, needed by every shard for the warp and base_feat), then the fusion
+        statistics of frames [first_frame, n).  Returns (stats [B,H,W,3C] fp32 -- the plan's static
+        buffer, overwritten by the next call -- and offsets [B,n-1,2,H,W])."""
+        self._ready(burst)
+        B, N, _, H, W = burst.shape
+        if N < 2:
+            raise ValueError('a frame shard needs the reference frame and at least one other frame')
+        key = ('partial', B, N, H, W, int(first_frame))
+        plan = self.plans.get(key)
+        if plan is None:
+            plan = self.plans[key] = self._build(B, N, H, W, mode='partial', first_frame=int(first_frame))
+        plan.bufs['burst'].copy_(burst.to(torch.float32), non_blocking=True)
+        plan.run(L.stream_ptr(burst.device))
+        return plan.bufs['stats'], plan.bufs['offsets'].view(B, N - 1, 2, H, W)
+
+    def gathered_buffer(self, R, B, H, W):
+        """The combine plan's input buffer [R,B,H,W,3C] fp32: all-gather the ranks' stats straight into it."""
+        if self.device is None:
+            raise RuntimeError('gathered_buffer: run forward_partial first (the engine packs its weights there)')
+        key = ('combine', R, B, H, W)
+        plan = self.plans.get(key)
+        if plan is None:
+            plan = self.plans[key] = self._build_combine(R, B, H, W)
+        return plan.bufs['gathered']
+
+    def combine_decode(self, gathered):
+        """Log-sum-exp combine of gathered [R,B,H,W,3C] statistics + decoder -> pred [B,3,sH,sW] (clone)."""
+        self._ready(gathered)
+        R, B, H, W = gathered.shape[:4]
+        buf = self.gathered_buffer(R, B, H, W)
+        if buf.data_ptr() != gathered.data_ptr():
+            buf.copy_(gathered, non_blocking=True)
+        plan = self.plans[('combine', R, B, H, W)]
+        plan.run(L.stream_ptr(gathered.device))
+        return plan.bufs['pred'].clone()
 
 
 # ==================================================================================================

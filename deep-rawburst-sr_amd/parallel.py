@@ -50,3 +50,43 @@ def run_sharded(net, bursts):
     local = shard(bursts)
     pred, _ = net(local)
     return gather_predictions(pred, bursts.shape[0])
+
+
+# ---------------------------------------------------------------------------------------------------
+# Frame sharding (BASELINE configs[4]): the frames of each burst split over ranks.
+# Encoder, PWC-Net alignment and warp are per frame; every rank also holds the reference frame (the
+# warp target and base_feat_proj, merging.py:80, need it).  The one coupling point is the softmax over
+# the burst (merging.py:116-124): each rank reduces its own frames to (max, sum exp, sum exp*feat)
+# statistics, one all-gather moves them (3*C*H*W fp32 per burst per rank -- instead of gathering the
+# warped 512-channel features of every frame), and a log-sum-exp combine rebuilds the fused embedding.
+# The decoder then runs on every rank (redundant, it is per burst).
+# ---------------------------------------------------------------------------------------------------
+def frame_shard(num_frames, rank, world):
+    """Frame indices rank `rank` processes: [0] + its contiguous share of frames 1..N-1, and the first
+    local index whose statistics it contributes (0 on rank 0, which owns the reference frame; 1 elsewhere,
+    so frame 0 enters the softmax exactly once)."""
+    if not 1 <= world <= num_frames - 1:
+        raise ValueError(f'frame sharding needs 1 <= world ({world}) <= N-1 ({num_frames - 1})')
+    a, b = shard_range(num_frames - 1, rank, world)
+    return [0] + list(range(1 + a, 1 + b)), (0 if rank == 0 else 1)
+
+
+def frame_sharded_forward(net, burst, partial_fn=None, combine_fn=None, gathered_fn=None):
+    """pred [B,3,sH,sW] of `burst` [B,N,4,H,W] (same on every rank) with its frames sharded over the
+    process group.  partial_fn(local_burst, first) -> stats and combine_fn(gathered [R,...]) -> pred
+    default to the HIP engine (DBSREngine.forward_partial / combine_decode); gathered_fn(R, stats) gives
+    the all-gather destination (the engine's combine input buffer, so the collective writes in place)."""
+    rank, world = dist.get_rank(), dist.get_world_size()
+    frames, first = frame_shard(burst.shape[1], rank, world)
+    local = burst[:, frames]
+    if partial_fn is None:
+        eng = net._get_engine()
+        partial_fn = lambda x, f: eng.forward_partial(x, f)[0]                          # noqa: E731
+        combine_fn = eng.combine_decode
+        gathered_fn = lambda R, st: eng.gathered_buffer(R, *st.shape[:3])              # noqa: E731
+    stats = partial_fn(local, first)
+    gathered = gathered_fn(world, stats) if gathered_fn is not None else \
+        stats.new_empty((world,) + tuple(stats.shape))
+    # concatenated along dim 0 ([R*B,...] view of the [R,B,...] buffer): the layout gloo and RCCL both take
+    dist.all_gather_into_tensor(gathered.view((-1,) + tuple(stats.shape[1:])), stats.contiguous())
+    return combine_fn(gathered)

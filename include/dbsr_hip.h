@@ -16,6 +16,7 @@
  *   dbsr_backwarp             models/alignment/pwcnet.py:16-38 (backwarp)
  *   dbsr_warp_bilinear        models/layers/warp.py:19-46 (warp), called at models/dbsr/encoders.py:80
  *   dbsr_fuse_softmax         models/dbsr/merging.py:116-126 (softmax over the burst + weighted sum)
+ *   dbsr_fuse_partial/combine the same softmax-fusion split over frame-sharded ranks (log-sum-exp combine)
  *   dbsr_conv2d               nn.Conv2d (+ReLU/LeakyReLU, ResBlock residual, PixelShuffle epilogue)
  *                             as composed by models/layers/blocks.py:46-96, upsampling.py:51-58,
  *                             models/alignment/pwcnet.py:45-207, models/dbsr/{encoders,merging,decoders}.py
@@ -37,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DBSR_ABI_VERSION 3
+#define DBSR_ABI_VERSION 4
 
 enum { DBSR_F32 = 0, DBSR_BF16 = 1 };
 enum { DBSR_ACT_NONE = 0, DBSR_ACT_RELU = 1, DBSR_ACT_LRELU = 2 };      /* LeakyReLU slope 0.1 */
@@ -143,6 +144,16 @@ int dbsr_warp_bilinear(int n, int h, int w, int c, dbsr_tensor feat, const float
  * weights (optional, ptr NULL to skip): NHWC images b*N+n.  fused: NHWC images b. */
 int dbsr_fuse_softmax(int B, int N, int hw, int c, dbsr_tensor logits, dbsr_tensor ref, dbsr_tensor oth,
                       dbsr_tensor fused, dbsr_tensor weights, void* stream);
+
+/* Frame-sharded fusion (the softmax over the burst of models/dbsr/merging.py:116-124
+ * split over ranks holding disjoint frame subsets).  dbsr_fuse_partial: statistics of the local frames
+ * n in [first_frame, N) (same logits/ref/oth addressing as dbsr_fuse_softmax) into stats, fp32
+ * [B][hw][3c] = (m = max_n l | s = sum e^(l-m) | a = sum e^(l-m) f).  dbsr_fuse_combine: R such blocks
+ * laid out back to back (an all-gather of the ranks' stats) -> fused = sum_r a_r e^(m_r-M) /
+ * sum_r s_r e^(m_r-M), M = max_r m_r; equal to the unsharded fusion up to fp32 rounding order. */
+int dbsr_fuse_partial(int B, int N, int hw, int c, int first_frame, dbsr_tensor logits, dbsr_tensor ref,
+                      dbsr_tensor oth, float* stats, void* stream);
+int dbsr_fuse_combine(int R, int B, int hw, int c, const float* stats, dbsr_tensor fused, void* stream);
 
 /* ConvTranspose2d(cin -> cout<=4, k=4, s=2, p=1): in NHWC slice [n][h][w], out NHWC fp32 [n][2h][2w].
  * w: fp32 repacked as [ky][kx][cout][cin8] (torch's [cin][cout][4][4] permuted, channels zero-padded

@@ -244,7 +244,7 @@ def encoder(x, sd, kw, zero_flow=False):
             'offsets': offsets}
 
 
-def merging(x, sd, kw):
+def merging(x, sd, kw, return_logits=False):
     """WeightedSum.forward (merging.py:61-127) with use_offset=True, offset_modulo=1.0,
     ref_offset_noise=0, softmax=True, use_base_frame=True (dbsrnet.py:47-53 defaults)."""
     ref_feat = x['ref_feat'][:, :1].contiguous()
@@ -269,9 +269,37 @@ def merging(x, sd, kw):
         w = res_block(w, sd, f'merging.weight_predictor.{i}')
     w = conv_block(w, sd, f'merging.weight_predictor.{nres + 1}', act='none')
     w = w.view(shape[0], -1, *w.shape[-3:])
+    if return_logits:
+        return all_feat, w
     wn = F.softmax(w, dim=1)
     fused = (all_feat * wn).sum(dim=1)
     return {'fused_enc': fused, 'fusion_weights': wn}
+
+
+def fuse_partial_stats(all_feat, logits, first):
+    """Frame-sharded fusion, rank-local half (splits merging.py:116-124): over frames
+    n >= first of this shard, m = max l, s = sum e^(l-m), a = sum e^(l-m) f.  Layout [B,H,W,3C]
+    (m | s | a), the one dbsr_fuse_partial writes."""
+    lg, f = logits[:, first:], all_feat[:, first:]
+    B, _, C, H, W = all_feat.shape
+    if lg.shape[1] == 0:
+        m = torch.full((B, C, H, W), float('-inf'), dtype=logits.dtype)
+        s = torch.zeros(B, C, H, W, dtype=logits.dtype)
+        a = torch.zeros(B, C, H, W, dtype=logits.dtype)
+    else:
+        m = lg.max(dim=1).values
+        e = torch.exp(lg - m.unsqueeze(1))
+        s, a = e.sum(dim=1), (e * f).sum(dim=1)
+    return torch.cat([m, s, a], dim=1).permute(0, 2, 3, 1).contiguous()
+
+
+def fuse_combine(gathered):
+    """Log-sum-exp combine of gathered [R,B,H,W,3C] statistics -> fused [B,C,H,W] (dbsr_fuse_combine)."""
+    C = gathered.shape[-1] // 3
+    m, s, a = gathered[..., :C], gathered[..., C:2 * C], gathered[..., 2 * C:]
+    M = m.max(dim=0).values
+    k = torch.where(torch.isinf(m), torch.zeros_like(m), torch.exp(m - M.unsqueeze(0)))
+    return ((a * k).sum(0) / (s * k).sum(0)).permute(0, 3, 1, 2).contiguous()
 
 
 def decoder(x, sd, kw):

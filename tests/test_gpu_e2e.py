@@ -108,3 +108,25 @@ def test_compute_score_hip_vs_oracle(tmp_path, synth_sd):
         r = float(psnr(ev.quantize_prediction(ref), g.unsqueeze(0)))
         print(meta['burst_name'], mine['per_image'][meta['burst_name']], r)
         assert abs(mine['per_image'][meta['burst_name']] - r) <= 0.01
+
+
+@pytest.mark.parametrize('world', [1, 2, 3])
+def test_frame_sharded_fusion_hip(golden, synth_sd, world):
+    """configs[4]'s frame-sharded path on one device: each simulated rank runs forward_partial on its
+    frame shard (dbsr_fuse_partial), the statistics are stacked as the all-gather would lay them out, and
+    combine_decode (dbsr_fuse_combine + decoder) must reproduce the reference forward (fp32, 1e-3)."""
+    from dbsr_amd.parallel import frame_shard
+    g = golden('e2e_b1n4')
+    burst = torch.from_numpy(g['burst']).to(DEV)
+    net = _net(synth_sd, torch.float32)
+    eng = net._get_engine()
+    B, N, _, H, W = burst.shape
+    with torch.no_grad():
+        stats = []
+        for r in range(world):
+            frames, first = frame_shard(N, r, world)
+            st, _ = eng.forward_partial(burst[:, frames], first)
+            stats.append(st.clone())
+        pred = eng.combine_decode(torch.stack(stats)).cpu()
+    np.testing.assert_allclose(pred[..., 100:164, 100:164].numpy(), g['pred_crop'], atol=1e-3, rtol=0)
+    np.testing.assert_allclose(pred.double().sum(dim=(-2, -1)).numpy(), g['pred_sum'], rtol=1e-4)

@@ -62,3 +62,67 @@ def test_gloo_world2_shard_gather_and_timing():
     assert [r[1] for r in res] == [3, 2]          # 5 bursts over 2 ranks
     assert all(r[2] for r in res)                  # gathered predictions == single-process result
     assert all(abs(r[3] - 1.5) < 1e-12 for r in res)   # max over ranks
+
+
+def test_frame_shard_assignment():
+    from dbsr_amd.parallel import frame_shard
+    for N in [2, 4, 14]:
+        for world in range(1, N):
+            seen = []
+            for r in range(world):
+                frames, first = frame_shard(N, r, world)
+                assert frames[0] == 0 and len(frames) >= 2
+                assert first == (0 if r == 0 else 1)
+                seen += frames[first:]
+            assert sorted(seen) == list(range(N))      # every frame enters the softmax exactly once
+    with pytest.raises(ValueError):
+        frame_shard(4, 0, 4)
+
+
+def _frame_worker(rank, world, port, q):
+    """Frame-sharded forward over gloo with the oracle standing in for the HIP kernels (the product's
+    kernels are checked against the same restatement on the GPU, tests/test_gpu_e2e.py)."""
+    import torch.distributed as dist
+    from dbsr_amd import parallel
+    from dbsr_amd.burst import synthetic_bursts
+    from dbsr_amd.weights import generate_state_dict
+    import dbsr_amd
+    from dbsr_amd import arch
+    from oracle import dbsr_oracle as orc
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        torch.set_num_threads(2)
+        net = dbsr_amd.dbsrnet_cvpr2021(**dbsr_amd.DBSR_SYNTHETIC_KWARGS)
+        sd = orc.state_dict_to_torch(generate_state_dict(arch.state_dict_shapes(net), seed=0))
+        kw = orc.DBSR_SYNTHETIC_KWARGS
+        burst, _ = synthetic_bursts(1, 4, 24, 24, sr_factor=8, seed=4)
+
+        def partial_fn(local, first):
+            all_feat, logits = orc.merging(orc.encoder(local, sd, kw), sd, kw, return_logits=True)
+            return orc.fuse_partial_stats(all_feat, logits, first)
+
+        def combine_fn(gathered):
+            return orc.decoder({'fused_enc': orc.fuse_combine(gathered)}, sd, kw)
+        pred = parallel.frame_sharded_forward(None, burst, partial_fn, combine_fn)
+        if rank == 0:
+            ref, _ = orc.dbsr_forward(burst, sd)
+            q.put((rank, float((pred - ref).abs().max())))
+        else:
+            q.put((rank, 0.0))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_frame_sharded_fusion():
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_frame_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res[0][1] <= 1e-4, res            # sharded == unsharded forward (fp32, rounding order only)
