@@ -1275,6 +1275,124 @@ ConvK make_convk(const dbsr_conv_desc* d) {
     return k;
 }
 
+// ------------------------------------------------------------------------------------------------
+// Warp + feature projection in one pass (encoders.py:80 then merging.py:76-78 on the warped frames):
+// the bilinear warp of a 16-pixel tile (4 waves x 4 pixels, the warp512 data flow: 16-B lanes, all
+// 16 tap loads in flight) is written to HBM (the fusion still needs it) AND to a padded LDS tile,
+// from which each wave runs the 1x1 512 -> 64 projection for 16 output channels on MFMA
+// (16 k-steps of 16x16x32 bf16; its A operand -- the wave's 16 weight rows, 64 VGPRs -- stays in
+// registers for the whole persistent loop).  Saves re-reading the warped features (P*HW*1 KiB) for
+// the projection.  Tiles are dealt in contiguous runs per XCD so a tap's neighbour rows hit the same
+// L2.  Same MFMA k-order as the generic conv on the same bf16 inputs.
+// ------------------------------------------------------------------------------------------------
+#ifndef DBSR_WARP_PROJ_PPW
+#define DBSR_WARP_PROJ_PPW 4
+#endif
+constexpr int WP_ROW = 512 + 8;   // LDS row pitch (bf16): +16 B keeps the 16 rows of a b128 read on distinct banks
+template <int PPW>
+__global__ __launch_bounds__(256, 2) void warp_proj_kernel(int n, int h, int w, dbsr_tensor feat,
+                                                           const float* __restrict__ flow, long long fis,
+                                                           dbsr_tensor out, ConvK k, int ntiles) {
+    constexpr int TP = 4 * PPW;   // pixels per tile
+    __shared__ __attribute__((aligned(16))) bf16_t tile[TP * WP_ROW];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int col = lane & 15, kgl = lane >> 4;
+    const int hw = h * w;
+    const unsigned total = (unsigned)n * hw;
+    // XCD-aware contiguous tile runs: logical block lb (grouped by XCD) owns tiles [t0, t1)
+    const unsigned b = blockIdx.x, nb = gridDim.x, xcd = b & 7, q8 = nb >> 3, r8 = nb & 7;
+    const unsigned lb = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+    const int t0 = (int)((long long)ntiles * lb / nb), t1 = (int)((long long)ntiles * (lb + 1) / nb);
+    const bool mm = wave * 16 < k.cout;
+    Frag<bf16_t> A[16];
+    const bf16_t* wrow = (const bf16_t*)k.w + (long long)(wave * 16 + col) * k.Kp + kgl * 8;
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) {
+        if (mm) A[ks].load(wrow + ks * 32);
+        else A[ks].zero();
+    }
+    const f32x4_t bias = load_bias4(k, wave * 16 + kgl * 4);
+    // software pipeline: the next tile's 16 tap loads per lane are in flight while this tile's
+    // projection (MFMA + epilogue) runs
+    struct Taps {
+        u32x4_t v[PPW][4];
+        float tw[PPW][4];
+        bf16_t* obase[PPW];
+        bool live[PPW];
+    };
+    auto issue = [&](int t, Taps& T) {
+#pragma unroll
+        for (int i = 0; i < PPW; ++i) {
+            const unsigned pix = (unsigned)t * TP + wave * PPW + i;
+            T.live[i] = pix < total;
+            const unsigned pc = T.live[i] ? pix : 0;
+            const int p = (int)(pc / hw), rr = (int)(pc - (unsigned)p * hw);
+            const int y = rr / w, x = rr - y * w;
+            const float* fl = flow + (long long)p * fis + rr;
+            const float gx = ((float)x + 0.5f) + fl[0];
+            const float gy = ((float)y + 0.5f) + fl[hw];
+            const float gxn = 2.0f * gx / (float)w - 1.0f, gyn = 2.0f * gy / (float)h - 1.0f;
+            const float ix = ((gxn + 1.f) * (float)w - 1.f) / 2.f;
+            const float iy = ((gyn + 1.f) * (float)h - 1.f) / 2.f;
+            const float fx0 = floorf(ix), fy0 = floorf(iy);
+            const int x0 = (int)fx0, y0 = (int)fy0;
+            const float wx1 = ix - fx0, wx0 = 1.f - wx1, wy1 = iy - fy0, wy0 = 1.f - wy1;
+            const bf16_t* fb = img_ptr<bf16_t>(feat, p) + lane * 8;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int xx = x0 + (q & 1), yy = y0 + (q >> 1);
+                const bool ok = (unsigned)xx < (unsigned)w && (unsigned)yy < (unsigned)h;
+                T.tw[i][q] = ok ? ((q & 1) ? wx1 : wx0) * ((q >> 1) ? wy1 : wy0) : 0.f;
+                T.v[i][q] = *(const u32x4_t*)(fb + (ok ? (yy * w + xx) * feat.ld : 0));
+            }
+            T.obase[i] = img_ptr<bf16_t>(out, p) + (long long)rr * out.ld + lane * 8;
+        }
+    };
+    Taps cur;
+    if (t0 < t1) issue(t0, cur);
+    for (int t = t0; t < t1; ++t) {
+        // ---- warp PPW pixels per wave ----
+#pragma unroll
+        for (int i = 0; i < PPW; ++i) {
+            f32x2_t acc[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const f32x2_t w2 = {cur.tw[i][q], cur.tw[i][q]};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const f32x2_t x2 = {__uint_as_float(cur.v[i][q][e] << 16),
+                                        __uint_as_float(cur.v[i][q][e] & 0xffff0000u)};
+                    acc[e] = __builtin_elementwise_fma(w2, x2, acc[e]);
+                }
+            }
+            u32x4_t o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = pack_bf16x2(acc[e][0], acc[e][1]);
+            if (cur.live[i]) *(u32x4_t*)cur.obase[i] = o;
+            *(u32x4_t*)(tile + (wave * PPW + i) * WP_ROW + lane * 8) = o;
+        }
+        __syncthreads();
+        if (t + 1 < t1) issue(t + 1, cur);
+        // ---- 1x1 projection of the 16 warped pixels: wave -> output channels [16*wave, 16*wave+16) ----
+        if (mm) {
+#pragma unroll
+            for (int cb = 0; cb < TP / 16; ++cb) {
+                f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int ks = 0; ks < 16; ++ks) {
+                    Frag<bf16_t> B;
+                    B.v = *(const bf16x8_t*)(tile + (cb * 16 + col) * WP_ROW + ks * 32 + kgl * 8);
+                    acc = mma(A[ks], B, acc);
+                }
+                const int p = t * TP + cb * 16 + col;
+                if (p < k.npix && wave * 16 + kgl * 4 < k.cout)
+                    epilogue_px<bf16_t>(k, p, wave * 16 + kgl * 4, acc, bias);
+            }
+        }
+        __syncthreads();
+    }
+}
+
 }  // namespace
 
 extern "C" int dbsr_conv_kernel_for(const dbsr_conv_desc* d) {
@@ -1404,3 +1522,34 @@ extern "C" int dbsr_debug_pipe_stamps_clear() {
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_pipe_stamps), zeros, sizeof(zeros), 0, hipMemcpyHostToDevice);
 }
 #endif
+
+extern "C" int dbsr_warp_proj(int n, int h, int w, dbsr_tensor feat, const float* flow, long long flow_img_stride,
+                              dbsr_tensor out, const dbsr_conv_desc* d, void* stream) {
+    DBSR_CHECK_ARG(d && feat.ptr && flow && out.ptr && d->w && d->y.ptr, "warp_proj: null pointer");
+    DBSR_CHECK_ARG(feat.dtype == DBSR_BF16 && out.dtype == DBSR_BF16 && d->x.dtype == DBSR_BF16 &&
+                   d->y.dtype == DBSR_BF16, "warp_proj: bf16 only");
+    DBSR_CHECK_ARG(n > 0 && h > 0 && w > 0 && (long long)n * h * w < (1LL << 31), "warp_proj: bad sizes");
+    DBSR_CHECK_ARG(feat.ld % 8 == 0 && feat.c0 % 8 == 0 && out.ld % 8 == 0 && out.c0 % 8 == 0 &&
+                   feat.map.fpg > 0 && out.map.fpg > 0, "warp_proj: feat/out ld, c0 multiples of 8, fpg > 0");
+    // the projection must read exactly the warped tensor
+    DBSR_CHECK_ARG(d->x.ptr == out.ptr && d->x.ld == out.ld && d->x.c0 == out.c0 &&
+                   d->x.img_stride == out.img_stride && d->x.map.fpg == out.map.fpg &&
+                   d->x.map.group_stride == out.map.group_stride && d->x.map.group_offset == out.map.group_offset &&
+                   d->x.map.inner_stride == out.map.inner_stride, "warp_proj: desc->x must be the warp output");
+    DBSR_CHECK_ARG(d->n_frames == n && d->in_h == h && d->in_w == w && d->out_h == h && d->out_w == w &&
+                   d->cin == 512 && d->kh == 1 && d->kw == 1 && d->stride == 1 && d->pad == 0 && d->dil == 1 &&
+                   d->cout > 0 && d->cout <= 64 && d->cout % 4 == 0 && !d->res.ptr && !d->precise &&
+                   d->out_mode == DBSR_OUT_NHWC && d->y.map.fpg > 0 && d->y.c0 + d->cout <= d->y.ld,
+                   "warp_proj: projection must be a 1x1 512 -> <=64 NHWC conv over the warped frames");
+    ConvK k = make_convk(d);
+    DBSR_CHECK_ARG(k.Kp == 512, "warp_proj: packed K %d != 512", k.Kp);
+    constexpr int PPW = DBSR_WARP_PROJ_PPW;
+    const int ntiles = (int)(((long long)n * h * w + 4 * PPW - 1) / (4 * PPW));
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int grid = std::min(ntiles, 2 * cus);
+    hipLaunchKernelGGL(warp_proj_kernel<PPW>, dim3(grid), dim3(256), 0, (hipStream_t)stream, n, h, w, feat, flow,
+                       flow_img_stride, out, k, ntiles);
+    DBSR_LAUNCH_CHECK();
+    return 0;
+}

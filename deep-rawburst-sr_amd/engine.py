@@ -412,6 +412,10 @@ class DBSREngine:
     CU_SPLIT = int(os.environ.get('DBSR_CU_SPLIT', '0'))
     # bf16: fuse the RGB predictor into the last decoder ResBlock conv (DBSR_FUSED_HEAD=0: separate kernel)
     FUSED_HEAD = os.environ.get('DBSR_FUSED_HEAD', '1') == '1'
+    # bf16: warp + feature projection of the warped frames in one kernel (dbsr_warp_proj).  Off by
+    # default: measured 209-215 us vs 108 + 93 us for the two kernels at cfg2 (its 64 weight VGPRs cap
+    # it at 2 waves/SIMD, half the tap loads in flight of the standalone warp); DBSR_WARP_PROJ=1 enables
+    WARP_PROJ = os.environ.get('DBSR_WARP_PROJ', '0') == '1'
 
     def __init__(self, net):
         self.net = net
@@ -559,7 +563,19 @@ class DBSREngine:
             plan.add('warp', lib.dbsr_warp_bilinear, P, H, W, C, E.d(0, (N - 1, N, 1, 1)), bufs['offsets'].data_ptr(),
                      2 * H * W, Wf.d(0), work=('byte', 2.0 * P * C * H * W * es + 8.0 * P * H * W))
         if P > 0:
-            plan.conv('merge.proj_oth', self.proj, P, Wf, 0, hw, PJ, 0, L.ACT_RELU, ymap=(N - 1, N, 1, 1))
+            d = plan.conv('merge.proj_oth', self.proj, P, Wf, 0, hw, PJ, 0, L.ACT_RELU, ymap=(N - 1, N, 1, 1))
+            if dt == torch.bfloat16 and C == 512 and pd <= 64 and DBSREngine.WARP_PROJ:
+                # one kernel for the warp and the projection of its output (dbsr_warp_proj): replaces the
+                # two ops just emitted; reported as the 'warp' family (bytes: warp + projection output)
+                assert plan.ops[-2][2] == 'warp' and plan.ops[-1][2] == 'merge.proj_oth'
+                wbytes = plan.work[len(plan.ops) - 2][1] + 2.0 * P * H * W * pd
+                for _ in range(2):
+                    plan.ops.pop()
+                    plan.work.pop(len(plan.ops), None)
+                    plan.kernel.pop(len(plan.ops), None)
+                plan.add('warp+proj', lib.dbsr_warp_proj, P, H, W, E.d(0, (N - 1, N, 1, 1)),
+                         bufs['offsets'].data_ptr(), 2 * H * W, Wf.d(0), ctypes.byref(d), work=('byte', wbytes))
+                plan.kernel[len(plan.ops) - 1] = 'warp'
         plan.add('merge.prep', lib.dbsr_merge_prep, B, N, H * W, pd, PJ.d(0), WP.d(0))
         q = [NHWC(F, H, W, self.wp_init.cout, dt, dev) for _ in range(3)]
         plan.conv('merge.wp.init', self.wp_init, F, WP, 0, hw, q[0], 0, L.ACT_RELU)

@@ -15,6 +15,7 @@
  *                             :385) incl. the leaky_relu applied by its callers, pwcnet.py:161,169
  *   dbsr_backwarp             models/alignment/pwcnet.py:16-38 (backwarp)
  *   dbsr_warp_bilinear        models/layers/warp.py:19-46 (warp), called at models/dbsr/encoders.py:80
+ *   dbsr_warp_proj            the warp + merging.py:76-78 (1x1 feat_project_layer of the warped frames)
  *   dbsr_fuse_softmax         models/dbsr/merging.py:116-126 (softmax over the burst + weighted sum)
  *   dbsr_fuse_partial/combine the same softmax-fusion split over frame-sharded ranks (log-sum-exp combine)
  *   dbsr_conv2d               nn.Conv2d (+ReLU/LeakyReLU, ResBlock residual, PixelShuffle epilogue)
@@ -38,7 +39,7 @@
 extern "C" {
 #endif
 
-#define DBSR_ABI_VERSION 4
+#define DBSR_ABI_VERSION 5
 
 enum { DBSR_F32 = 0, DBSR_BF16 = 1 };
 enum { DBSR_ACT_NONE = 0, DBSR_ACT_RELU = 1, DBSR_ACT_LRELU = 2 };      /* LeakyReLU slope 0.1 */
@@ -138,6 +139,13 @@ int dbsr_backwarp(int n, int h, int w, int c, dbsr_tensor in, dbsr_tensor flow, 
  * [n][2][h][w] (the `offsets` tensor), flow_img_stride elements per image. */
 int dbsr_warp_bilinear(int n, int h, int w, int c, dbsr_tensor feat, const float* flow,
                        long long flow_img_stride, dbsr_tensor out, void* stream);
+
+/* dbsr_warp_bilinear (bf16, 512 channels) fused with the 1x1 feature projection that consumes its
+ * output (merging.py:76-78, feat_project_layer on the warped frames): out receives the warped
+ * features exactly as dbsr_warp_bilinear writes them, and d (a 1x1 cin=512 -> cout<=64 NHWC conv
+ * whose x is `out`, bias/act as usual, no residual) is applied to them in the same pass. */
+int dbsr_warp_proj(int n, int h, int w, dbsr_tensor feat, const float* flow, long long flow_img_stride,
+                   dbsr_tensor out, const dbsr_conv_desc* d, void* stream);
 
 /* Softmax over the burst of logits[b,n] and weighted sum of feats[b,n].  Frame (b,n): logits image
  * b*N+n; feature image: n==0 -> ref (map applied to b), n>0 -> oth (map applied to b*(N-1)+n-1).

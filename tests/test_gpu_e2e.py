@@ -130,3 +130,26 @@ def test_frame_sharded_fusion_hip(golden, synth_sd, world):
         pred = eng.combine_decode(torch.stack(stats)).cpu()
     np.testing.assert_allclose(pred[..., 100:164, 100:164].numpy(), g['pred_crop'], atol=1e-3, rtol=0)
     np.testing.assert_allclose(pred.double().sum(dim=(-2, -1)).numpy(), g['pred_sum'], rtol=1e-4)
+
+
+def test_warp_proj_fused_matches_two_kernels(golden, synth_sd):
+    """dbsr_warp_proj (warp + 1x1 projection in one kernel) against dbsr_warp_bilinear followed by the
+    generic 1x1 conv: same bf16 inputs, same MFMA k-order -> bitwise identical forward."""
+    from dbsr_amd.engine import DBSREngine
+    g = golden('e2e_b1n14')
+    burst = torch.from_numpy(g['burst']).to(DEV)
+    outs = []
+    old = DBSREngine.WARP_PROJ
+    try:
+        for flag in (True, False):
+            DBSREngine.WARP_PROJ = flag
+            net = _net(synth_sd, torch.bfloat16)
+            with torch.no_grad():
+                pred, aux = net(burst)
+            names = [op[2] for op in net._engine.plans[tuple(burst.shape[i] for i in (0, 1, 3, 4))].ops]
+            assert ('warp+proj' in names) == flag
+            outs.append((pred.clone(), aux['fusion_weights'].clone()))
+    finally:
+        DBSREngine.WARP_PROJ = old
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
