@@ -19,6 +19,7 @@
 #include "common.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 
 using namespace dbsr;
 
@@ -48,6 +49,7 @@ struct ConvK {
     const float* head_w; // fused 1x1 head (pipelined kernel, EPI 4): fp32 [head_cout][cout], bias [head_cout]
     const float* head_b;
     int head_cout;       // y is then the head's fp32 NCHW output (y_is = image stride)
+    int stage_epi;       // generic kernel, MT == 4: LDS-staged 16-B-row epilogue (set by launch_conv)
 };
 
 template <typename T> struct Frag;
@@ -238,6 +240,42 @@ __global__ __launch_bounds__(256) void conv2d_kernel(ConvK k) {
         compute(a0, b0);
     }
 
+    // staged epilogue (bf16, plain NHWC, cout % 8 == 0): bias + act into a per-wave LDS tile, then each
+    // lane stores 16 B of a pixel row (MT*32 B per pixel), so a store instruction covers whole rows
+    // instead of the per-lane path's 8-B pieces scattered over 16 pixel rows (that path ran the Cin<=8
+    // input convs at ~1 TB/s)
+    if constexpr (sizeof(T) == 2 && sizeof(XT) == 2 && MT * NT >= 2) {
+        if (k.stage_epi) {
+            constexpr int PITCH = MT * 16 + 8;                     // bf16 per LDS row (+16 B: spreads banks)
+            constexpr int LPR = MT * 2;                            // lanes per pixel row (16 B each)
+            constexpr int RPI = 64 / LPR;                          // rows per store instruction
+            __shared__ __attribute__((aligned(16))) bf16_t stile[4][NT * 16 * PITCH];
+            bf16_t* st = stile[wave];
+#pragma unroll
+            for (int j = 0; j < NT; ++j)
+#pragma unroll
+                for (int i = 0; i < MT; ++i) {
+                    uint2 q;
+                    q.x = pack_bf16x2(apply_act(acc[i][j][0] + bias[i][0], k.act), apply_act(acc[i][j][1] + bias[i][1], k.act));
+                    q.y = pack_bf16x2(apply_act(acc[i][j][2] + bias[i][2], k.act), apply_act(acc[i][j][3] + bias[i][3], k.act));
+                    *(uint2*)(st + (j * 16 + col) * PITCH + i * 16 + kgl * 4) = q;
+                }
+            __syncthreads();
+            const int hw2 = k.out_h * k.out_w;
+            const int ch = (lane % LPR) * 8;
+#pragma unroll
+            for (int it = 0; it < NT * 16 / RPI; ++it) {
+                const int r = it * RPI + lane / LPR;
+                const int p = p_base + r;
+                if (p < k.npix && c_base + ch < k.cout) {
+                    const int f = p / hw2, rr = p - f * hw2;
+                    *(u32x4_t*)((T*)k.y + map_frame(k.ym, f) * k.y_is + (long long)rr * k.y_ld + k.y_c0 + c_base + ch) =
+                        *(const u32x4_t*)(st + r * PITCH + ch);
+                }
+            }
+            return;
+        }
+    }
     // epilogue: bias, activation, residual, post-activation, store (or fp32 partials under split-K)
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
@@ -1018,8 +1056,19 @@ int dispatch_pipe(int cfg, const ConvK& k, const dbsr_conv_desc* d, hipStream_t 
     return launch_pipe<32, 64, 8>(k, d->n_frames, s);
 }
 
+bool stage_epi_enabled() {     // DBSR_STAGE_EPI=0: per-lane epilogue everywhere (A/B runs)
+    static const bool on = [] {
+        const char* e = getenv("DBSR_STAGE_EPI");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
 template <typename T, int MT, int NT, typename XT = T>
-int launch_conv(const ConvK& k, hipStream_t s) {
+int launch_conv(const ConvK& k0, hipStream_t s) {
+    ConvK k = k0;
+    k.stage_epi = MT * NT >= 2 && sizeof(T) == 2 && sizeof(XT) == 2 && stage_epi_enabled() && k.ksplit == 1 &&
+                  k.out_mode == DBSR_OUT_NHWC && !k.y_f32 && !k.r && k.cout % 8 == 0 && k.y_ld % 8 == 0 &&
+                  k.y_c0 % 8 == 0 && k.head_cout == 0;
     dim3 grid((k.npix + 4 * NT * 16 - 1) / (4 * NT * 16), (k.cout + MT * 16 - 1) / (MT * 16), k.ksplit);
     hipLaunchKernelGGL((conv2d_kernel<T, MT, NT, XT>), grid, dim3(256), 0, s, k);
     DBSR_LAUNCH_CHECK();
@@ -1047,8 +1096,16 @@ int choose_ksplit(const ConvK& k, int mt, int nt) {
 size_t splitk_bytes(const ConvK& k, int sp) { return sp > 1 ? (size_t)sp * k.npix * k.cw * sizeof(float) : 0; }
 // generic kernel: the largest tile that still gives >= 2 blocks per CU (512 blocks); tiny PWC levels
 // (a few hundred pixels) fall through to 16 x 64-pixel tiles (and split-K) for parallelism
+int generic_min_blocks() {
+    static const int v = [] {
+        const char* e = getenv("DBSR_GENERIC_MIN_BLOCKS");
+        return e ? std::max(1, atoi(e)) : 512;
+    }();
+    return v;
+}
 void pick_generic_tile(const ConvK& k, int& best_m, int& best_n) {
     const int mts[3] = {4, 2, 1}, nts[3] = {4, 2, 1};
+    const long long minb = generic_min_blocks();
     best_m = 1;
     best_n = 1;
     for (int a = 0; a < 3; ++a) {
@@ -1056,7 +1113,7 @@ void pick_generic_tile(const ConvK& k, int& best_m, int& best_n) {
         for (int b = 0; b < 3; ++b) {
             const long long blocks = (long long)((k.npix + 64 * nts[b] - 1) / (64 * nts[b])) *
                                      ((k.cout + 16 * mts[a] - 1) / (16 * mts[a]));
-            if (blocks >= 512) {
+            if (blocks >= minb) {
                 best_m = mts[a];
                 best_n = nts[b];
                 return;
@@ -1272,6 +1329,7 @@ ConvK make_convk(const dbsr_conv_desc* d) {
     k.w_pipe = (const char*)d->w + (size_t)round_up(d->cout, 64) * k.Kp * esz;
     k.max_blocks = d->max_blocks;
     k.head_w = nullptr; k.head_b = nullptr; k.head_cout = 0;
+    k.stage_epi = 0;
     return k;
 }
 
