@@ -269,8 +269,8 @@ __global__ __launch_bounds__(256) void fuse_softmax_kernel(int B, int N, int hw,
 // twice the memory instructions).  All 2N loads are issued before the first use; the logits are
 // consumed once, so they are streamed with non-temporal loads, and the aux weights (written once,
 // never re-read by the forward) with non-temporal stores, keeping L2 for the feature rows.
-template <int NMAX>
-__global__ __launch_bounds__(256) void fuse512_bf16_kernel(int B, int N, int hw, dbsr_tensor logits, dbsr_tensor ref,
+template <int NMAX, bool RECOMP>
+__global__ __launch_bounds__(256, RECOMP ? 3 : 2) void fuse512_bf16_kernel(int B, int N, int hw, dbsr_tensor logits, dbsr_tensor ref,
                                                            dbsr_tensor oth, dbsr_tensor fused, dbsr_tensor weights) {
     const unsigned pix = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
     if (pix >= (unsigned)B * hw) return;
@@ -300,19 +300,25 @@ __global__ __launch_bounds__(256) void fuse512_bf16_kernel(int B, int N, int hw,
             }
         }
     }
-    float e[NMAX][8], s[8];
+    // RECOMP: exp() evaluated again in the weighting loop instead of keeping N x 8 fp32 values live
+    // (fewer VGPRs -> more waves per SIMD, at 2x the transcendental work)
+    float e[RECOMP ? 1 : NMAX][8], s[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) s[j] = 0.f;
 #pragma unroll
     for (int n = 0; n < NMAX; ++n) {
         if (n < N) {
+            float en[8];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                e[n][2 * j] = __expf(__uint_as_float(lr[n][j] << 16) - m[2 * j]);
-                e[n][2 * j + 1] = __expf(__uint_as_float(lr[n][j] & 0xffff0000u) - m[2 * j + 1]);
+                en[2 * j] = __expf(__uint_as_float(lr[n][j] << 16) - m[2 * j]);
+                en[2 * j + 1] = __expf(__uint_as_float(lr[n][j] & 0xffff0000u) - m[2 * j + 1]);
             }
 #pragma unroll
-            for (int j = 0; j < 8; ++j) s[j] += e[n][j];
+            for (int j = 0; j < 8; ++j) {
+                s[j] += en[j];
+                if constexpr (!RECOMP) e[n][j] = en[j];
+            }
         }
     }
     float inv[8], acc[8];
@@ -325,8 +331,16 @@ __global__ __launch_bounds__(256) void fuse512_bf16_kernel(int B, int N, int hw,
     for (int n = 0; n < NMAX; ++n) {
         if (n < N) {
             float wn[8];
+            if constexpr (RECOMP) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) wn[j] = e[n][j] * inv[j];
+                for (int j = 0; j < 4; ++j) {
+                    wn[2 * j] = __expf(__uint_as_float(lr[n][j] << 16) - m[2 * j]) * inv[2 * j];
+                    wn[2 * j + 1] = __expf(__uint_as_float(lr[n][j] & 0xffff0000u) - m[2 * j + 1]) * inv[2 * j + 1];
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) wn[j] = e[n][j] * inv[j];
+            }
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 acc[2 * j] = fmaf(__uint_as_float(fr[n][j] << 16), wn[2 * j], acc[2 * j]);
@@ -554,6 +568,15 @@ extern "C" int dbsr_warp_bilinear(int n, int h, int w, int c, dbsr_tensor feat, 
     });
 }
 
+// DBSR_FUSE_RECOMP=0: keep the exp() values live instead of recomputing them (A/B)
+static bool fuse_recomp() {
+    static const bool on = [] {
+        const char* e = getenv("DBSR_FUSE_RECOMP");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 // DBSR_FUSE512=0 selects the 4-channel kernel for A/B runs (default: the 512-channel bf16 kernel)
 static bool fuse512_enabled() {
     static const bool on = [] {
@@ -582,8 +605,12 @@ extern "C" int dbsr_fuse_softmax(int B, int N, int hw, int c, dbsr_tensor logits
                 (N == 1 || vec_ok(oth, 8)) && (!weights.ptr || (weights.dtype == DBSR_BF16 && vec_ok(weights, 8)))) {
                 const long long waves = (long long)B * hw;
 #define DBSR_FUSE512(NM)                                                                                       \
-    hipLaunchKernelGGL((fuse512_bf16_kernel<NM>), dim3(nblocks(waves, 4)), dim3(256), 0, (hipStream_t)stream, B, N, \
-                       hw, logits, ref, oth, fused, weights);
+    if (fuse_recomp())                                                                                         \
+        hipLaunchKernelGGL((fuse512_bf16_kernel<NM, true>), dim3(nblocks(waves, 4)), dim3(256), 0,             \
+                           (hipStream_t)stream, B, N, hw, logits, ref, oth, fused, weights);                   \
+    else                                                                                                       \
+        hipLaunchKernelGGL((fuse512_bf16_kernel<NM, false>), dim3(nblocks(waves, 4)), dim3(256), 0,            \
+                           (hipStream_t)stream, B, N, hw, logits, ref, oth, fused, weights);
                 if (N <= 4) {
                     DBSR_FUSE512(4)
                 } else if (N <= 8) {
