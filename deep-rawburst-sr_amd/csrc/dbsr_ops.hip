@@ -568,11 +568,13 @@ extern "C" int dbsr_warp_bilinear(int n, int h, int w, int c, dbsr_tensor feat, 
     });
 }
 
-// DBSR_FUSE_RECOMP=0: keep the exp() values live instead of recomputing them (A/B)
+// DBSR_FUSE_RECOMP=1: recompute exp() in the weighting loop at 3 waves/SIMD (~2 % faster, 150 vs 153 us,
+// but its 16 spilled VGPRs add ~65 MB of scratch traffic per launch, PMC r01f); default keeps the exp()
+// values live (2 waves/SIMD, HBM traffic = the algorithmic 812 MB)
 static bool fuse_recomp() {
     static const bool on = [] {
         const char* e = getenv("DBSR_FUSE_RECOMP");
-        return !(e && e[0] == '0');
+        return e && e[0] == '1';
     }();
     return on;
 }
