@@ -553,10 +553,17 @@ extern "C" int dbsr_warp_bilinear(int n, int h, int w, int c, dbsr_tensor feat, 
     return by_dtype(feat.dtype, [&](auto* tag) {
         using T = std::remove_pointer_t<decltype(tag)>;
         if (sizeof(T) == 2 && groups == 64) {
-            constexpr int PPW = 4;
-            const long long waves = ((long long)n * h * w + PPW - 1) / PPW;
-            hipLaunchKernelGGL((warp512_bf16_kernel<PPW>), dim3(nblocks(waves, 4)), dim3(256), 0, (hipStream_t)stream,
-                               n, h, w, feat, flow, flow_img_stride, out);
+            static const int ppw = [] {                      // DBSR_WARP_PPW (A/B): pixels per wave, 2/4/8
+                const char* e = getenv("DBSR_WARP_PPW");
+                return e ? atoi(e) : 4;
+            }();
+#define DBSR_WARP512(PPW)                                                                                      \
+    hipLaunchKernelGGL((warp512_bf16_kernel<PPW>), dim3(nblocks(((long long)n * h * w + PPW - 1) / PPW, 4)),  \
+                       dim3(256), 0, (hipStream_t)stream, n, h, w, feat, flow, flow_img_stride, out)
+            if (ppw == 2) DBSR_WARP512(2);
+            else if (ppw == 8) DBSR_WARP512(8);
+            else DBSR_WARP512(4);
+#undef DBSR_WARP512
         } else if (groups % 64 == 0)
             hipLaunchKernelGGL((warp_kernel<T, true>), dim3(nblocks((long long)n * h * w * groups, 256)), dim3(256), 0,
                                (hipStream_t)stream, n, h, w, groups, feat, flow, flow_img_stride, out);
