@@ -1451,6 +1451,141 @@ __global__ __launch_bounds__(256, 2) void warp_proj_kernel(int n, int h, int w, 
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// PixelShuffle upsampler + Gaussian blur in one kernel (upsampling.py:56-65: conv 1x1 Cin -> 64*32,
+// PixelShuffle(8), then the depthwise 3x3 Gaussian with zero padding).  Block = 8 waves over UB_TW
+// low-res pixels of one LR row y; the upsampled (bf16-rounded, exactly as the upsample kernel stores
+// it) HR tile rows 8y-1 .. 8y+8 and columns 8(x0-1) .. 8(x0+UB_TW)+7 are built in LDS -- row y's pixels
+// for all 64 sub-pixels, rows y-1 / y+1 only for the sub-row that borders the tile, LR pixels outside
+// the image as zeros (the blur's zero padding) -- then blurred from LDS with the blur kernel's tap
+// order and stored as whole 64-B pixels.  The 8*64*32*2 B per LR pixel intermediate never reaches HBM.
+// ------------------------------------------------------------------------------------------------
+constexpr int UB_TW = 8;
+constexpr int UB_COLS = (UB_TW + 2) * 8;                       // HR columns held (LR x0-1 .. x0+UB_TW)
+constexpr int UB_ROWB = UB_COLS * 64 + (UB_COLS / 8) * 16;     // bytes per HR row (16-B skew per 8 pixels)
+__device__ __forceinline__ int ub_off(int r, int c) { return r * UB_ROWB + c * 64 + (c >> 3) * 16; }
+
+struct K9f {
+    float k[9];
+};
+
+__global__ __launch_bounds__(512) void upsample_blur_kernel(ConvK k, K9f kk, int segs) {
+    __shared__ __attribute__((aligned(16))) unsigned char tile[10 * UB_ROWB];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int g = lane >> 4, col = lane & 15;
+    const int H = k.out_h, W = k.out_w;                     // low-res geometry
+    const int seg = blockIdx.x % segs;
+    const int rowid = blockIdx.x / segs;
+    const int y = rowid % H, f = rowid / H;
+    const int x0 = seg * UB_TW;
+    // pixel slots: group j (0: row y, 1: row y-1, 2: row y+1), slot col -> LR x = x0 - 1 + col
+    Frag<bf16_t> b[3][2];
+    bool valid[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const int yy = j == 0 ? y : (j == 1 ? y - 1 : y + 1);
+        const int xx = x0 - 1 + col;
+        valid[j] = col < UB_TW + 2 && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+        const bf16_t* xp = (const bf16_t*)k.x + map_frame(k.xm, f) * k.x_is +
+                           ((long long)(valid[j] ? yy : 0) * W + (valid[j] ? xx : 0)) * k.x_ld + g * 8;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            if (valid[j]) b[j][ks].load(xp + ks * 32);
+            else b[j][ks].zero();
+        }
+    }
+    const int m_row = 8 * (col >> 2) + (col & 3);
+    const int sx = wave;
+    // weights and bias of sub-pixel (sy, sx), prefetched one sub-row ahead (the loop is latency-bound
+    // on these L2 reads otherwise)
+    auto load_w = [&](int sy, Frag<bf16_t> (&a)[2][2], float4 (&bb)[2]) {
+        const int sub = sy * 8 + sx;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+                a[h][ks].load((const bf16_t*)k.w + (long long)(sub * 32 + m_row + 4 * h) * k.Kp + ks * 32 + g * 8);
+        if (k.bias) {
+            bb[0] = *(const float4*)(k.bias + sub * 32 + 8 * g);
+            bb[1] = *(const float4*)(k.bias + sub * 32 + 8 * g + 4);
+        } else {
+            bb[0] = make_float4(0.f, 0.f, 0.f, 0.f);
+            bb[1] = bb[0];
+        }
+    };
+    Frag<bf16_t> a_cur[2][2], a_nxt[2][2];
+    float4 bb_cur[2], bb_nxt[2];
+    load_w(0, a_cur, bb_cur);
+#pragma unroll 1
+    for (int sy = 0; sy < 8; ++sy) {
+        if (sy + 1 < 8) load_w(sy + 1, a_nxt, bb_nxt);
+        Frag<bf16_t> (&a)[2][2] = a_cur;
+        const float bv[8] = {bb_cur[0].x, bb_cur[0].y, bb_cur[0].z, bb_cur[0].w,
+                             bb_cur[1].x, bb_cur[1].y, bb_cur[1].z, bb_cur[1].w};
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            if (j == 1 && sy != 7) continue;            // row y-1: only its bottom sub-row borders the tile
+            if (j == 2 && sy != 0) continue;            // row y+1: only its top sub-row
+            f32x4_t acc[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                acc[h] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks) acc[h] = mma(a[h][ks], b[j][ks], acc[h]);
+            }
+            u32x4_t o = {0u, 0u, 0u, 0u};
+            if (valid[j]) {
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    o[e] = pack_bf16x2(apply_act(acc[0][2 * e] + bv[2 * e], k.act),
+                                       apply_act(acc[0][2 * e + 1] + bv[2 * e + 1], k.act));
+                    o[2 + e] = pack_bf16x2(apply_act(acc[1][2 * e] + bv[4 + 2 * e], k.act),
+                                           apply_act(acc[1][2 * e + 1] + bv[4 + 2 * e + 1], k.act));
+                }
+            }
+            const int r = j == 0 ? 1 + sy : (j == 1 ? 0 : 9);
+            if (col < UB_TW + 2) *(u32x4_t*)(tile + ub_off(r, col * 8 + sx) + g * 16) = o;
+        }
+        if (sy + 1 < 8) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks) a_cur[h][ks] = a_nxt[h][ks];
+            bb_cur[0] = bb_nxt[0];
+            bb_cur[1] = bb_nxt[1];
+        }
+    }
+    __syncthreads();
+    // blur: 8 HR rows x 8*UB_TW HR columns, 4 lanes (8 channels each) per HR pixel
+    const int Wh = W * 8;
+    bf16_t* ybase = (bf16_t*)k.y + map_frame(k.ym, f) * k.y_is + k.y_c0;
+#pragma unroll
+    for (int it = 0; it < 8 * 8 * UB_TW * 4 / 512; ++it) {
+        const int item = it * 512 + threadIdx.x;
+        const int px = item >> 2, q = item & 3;
+        const int pr = px / (8 * UB_TW), pc = px - pr * (8 * UB_TW);
+        const int X = x0 * 8 + pc;
+        if (X >= Wh) continue;
+        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int jj = 0; jj < 3; ++jj) {
+                const float kv = kk.k[i * 3 + jj];
+                const u32x4_t v = *(const u32x4_t*)(tile + ub_off(pr + i, 8 + pc - 1 + jj) + q * 16);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    acc[2 * e] = fmaf(kv, __uint_as_float(v[e] << 16), acc[2 * e]);
+                    acc[2 * e + 1] = fmaf(kv, __uint_as_float(v[e] & 0xffff0000u), acc[2 * e + 1]);
+                }
+            }
+        u32x4_t o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = pack_bf16x2(acc[2 * e], acc[2 * e + 1]);
+        *(u32x4_t*)(ybase + ((long long)(y * 8 + pr) * Wh + X) * k.y_ld + q * 8) = o;
+    }
+}
+
 }  // namespace
 
 extern "C" int dbsr_conv_kernel_for(const dbsr_conv_desc* d) {
@@ -1608,6 +1743,24 @@ extern "C" int dbsr_warp_proj(int n, int h, int w, dbsr_tensor feat, const float
     const int grid = std::min(ntiles, 2 * cus);
     hipLaunchKernelGGL(warp_proj_kernel<PPW>, dim3(grid), dim3(256), 0, (hipStream_t)stream, n, h, w, feat, flow,
                        flow_img_stride, out, k, ntiles);
+    DBSR_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int dbsr_upsample_blur(const dbsr_conv_desc* d, const float* k9, void* stream) {
+    DBSR_CHECK_ARG(d && k9 && d->x.ptr && d->w && d->y.ptr, "upsample_blur: null pointer");
+    DBSR_CHECK_ARG(d->x.ld % 8 == 0 && d->x.c0 % 8 == 0 && d->x.map.fpg > 0 && d->y.map.fpg > 0,
+                   "upsample_blur: bad input layout");
+    const ConvK k = make_convk(d);
+    DBSR_CHECK_ARG(use_upsample(d, k) && d->shuffle == 8 && k.Kp == 64 && k.cps == 32 && !d->res.ptr &&
+                   d->in_h == d->out_h && d->in_w == d->out_w && d->n_frames > 0,
+                   "upsample_blur: needs the bf16 1x1 Cin<=64 -> 64*32 PixelShuffle(8) upsampler");
+    DBSR_CHECK_ARG((long long)d->n_frames * d->out_h < (1LL << 24), "upsample_blur: too many rows");
+    K9f kk;
+    for (int i = 0; i < 9; ++i) kk.k[i] = k9[i];
+    const int segs = (d->out_w + UB_TW - 1) / UB_TW;
+    hipLaunchKernelGGL(upsample_blur_kernel, dim3((unsigned)(d->n_frames * d->out_h * segs)), dim3(512), 0,
+                       (hipStream_t)stream, k, kk, segs);
     DBSR_LAUNCH_CHECK();
     return 0;
 }

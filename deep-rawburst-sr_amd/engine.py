@@ -416,6 +416,11 @@ class DBSREngine:
     # default: measured 209-215 us vs 108 + 93 us for the two kernels at cfg2 (its 64 weight VGPRs cap
     # it at 2 waves/SIMD, half the tap loads in flight of the standalone warp); DBSR_WARP_PROJ=1 enables
     WARP_PROJ = os.environ.get('DBSR_WARP_PROJ', '0') == '1'
+    # bf16, x8: decoder upsampler + Gaussian blur in one kernel (dbsr_upsample_blur), bitwise equal to
+    # the two kernels.  Off by default: 82 us vs 40 + 39 us -- its LDS tile (4 KiB per low-res pixel)
+    # limits a block to 8 low-res pixels, so every block re-reads the whole 256-KiB weight matrix from
+    # L2 (8x the upsampler's amortisation).  DBSR_UPSAMPLE_BLUR=1 enables it.
+    UPSAMPLE_BLUR = os.environ.get('DBSR_UPSAMPLE_BLUR', '0') == '1'
 
     def __init__(self, net):
         self.net = net
@@ -621,10 +626,21 @@ class DBSREngine:
         i = self._resblocks(plan, 'dec.pre', self.dec_pre, B, hw, g, 0, dt)
         pc = self.dec_up.cout // (S * S)
         sh = [NHWC(B, H * S, W * S, pc, dt, dev) for _ in range(3)]
-        plan.conv('dec.upsample', self.dec_up, B, g[i], 0, hw, sh[0], 0, L.ACT_RELU, out_mode=L.OUT_SHUFFLE,
-                  shuffle=S)
         a = 0
-        if self.blur is not None:
+        if self.blur is not None and dt == torch.bfloat16 and S == 8 and DBSREngine.UPSAMPLE_BLUR:
+            # upsampler + blur in one kernel (dbsr_upsample_blur): the desc's y is the blurred output
+            kbuf = (ctypes.c_float * 9)(*self.blur)
+            plan.keep.append(kbuf)
+            d = plan.conv('dec.upsample+blur', self.dec_up, B, g[i], 0, hw, sh[1], 0, L.ACT_RELU,
+                          out_mode=L.OUT_SHUFFLE, shuffle=S)
+            fn, args, name, lane = plan.ops[-1]
+            plan.ops[-1] = (lib.dbsr_upsample_blur, (ctypes.byref(d), kbuf), name, lane)
+            plan.kernel[len(plan.ops) - 1] = 'conv1x1_shuffle'
+            a = 1
+        else:
+            plan.conv('dec.upsample', self.dec_up, B, g[i], 0, hw, sh[0], 0, L.ACT_RELU, out_mode=L.OUT_SHUFFLE,
+                      shuffle=S)
+        if self.blur is not None and a == 0:
             kbuf = (ctypes.c_float * 9)(*self.blur)
             plan.keep.append(kbuf)
             plan.add('dec.blur', lib.dbsr_gauss_blur3, B, H * S, W * S, pc, sh[0].d(0), kbuf, sh[1].d(0))

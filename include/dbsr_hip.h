@@ -26,6 +26,7 @@
  *   dbsr_flow_finalize        pwcnet.py:274-279 (x20 bilinear upsample + rescale) + merging.py:98-105
  *                             (offsets_all = cat(0, offsets) % offset_modulo)
  *   dbsr_gauss_blur3          upsampling.py:59-65 (depthwise Gaussian, zero padding)
+ *   dbsr_upsample_blur        upsampling.py:56-65 (PixelShuffle upsampler + Gaussian blur, one pass)
  *   dbsr_merge_prep           merging.py:79-89 (base_feat_proj, feat_diff_proj)
  *   dbsr_pwc_assemble         pwcnet.py:171 (cat([tenVolume, tenFirst, tenFlow, tenFeat]))
  */
@@ -39,7 +40,7 @@
 extern "C" {
 #endif
 
-#define DBSR_ABI_VERSION 5
+#define DBSR_ABI_VERSION 6
 
 enum { DBSR_F32 = 0, DBSR_BF16 = 1 };
 enum { DBSR_ACT_NONE = 0, DBSR_ACT_RELU = 1, DBSR_ACT_LRELU = 2 };      /* LeakyReLU slope 0.1 */
@@ -152,6 +153,12 @@ int dbsr_warp_proj(int n, int h, int w, dbsr_tensor feat, const float* flow, lon
  * weights (optional, ptr NULL to skip): NHWC images b*N+n.  fused: NHWC images b. */
 int dbsr_fuse_softmax(int B, int N, int hw, int c, dbsr_tensor logits, dbsr_tensor ref, dbsr_tensor oth,
                       dbsr_tensor fused, dbsr_tensor weights, void* stream);
+
+/* The decoder's PixelShuffle upsampler and Gaussian blur in one pass (upsampling.py:56-65): d is the
+ * bf16 1x1 conv (cin <= 64, cout = 64*32, shuffle 8, DBSR_OUT_SHUFFLE, packed with shuffle = 8) whose
+ * y is the BLURRED output; k9: the 3x3 kernel (host memory, row-major).  Equals dbsr_conv2d(d) into a
+ * temporary followed by dbsr_gauss_blur3 (same bf16 rounding of the intermediate). */
+int dbsr_upsample_blur(const dbsr_conv_desc* d, const float* k9, void* stream);
 
 /* Frame-sharded fusion (the softmax over the burst of models/dbsr/merging.py:116-124
  * split over ranks holding disjoint frame subsets).  dbsr_fuse_partial: statistics of the local frames
