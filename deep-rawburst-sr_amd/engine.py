@@ -120,6 +120,7 @@ class Plan:
         self.lanes = {0}
         self.streams = {}
         self.max_blocks = 0  # CU cap for lane-0 persistent convs issued while a side lane runs
+        self.side_max_blocks = int(os.environ.get('DBSR_SIDE_CUS', '0'))   # same for side-lane persistent convs
 
     def add(self, name, fn, *args, work=None):
         if work is not None:
@@ -174,7 +175,7 @@ class Plan:
         d.out_mode, d.shuffle = out_mode, shuffle
         d.workspace, d.workspace_bytes = None, 0
         d.precise = 1 if precise else 0
-        d.max_blocks = self.max_blocks if self.lane == 0 else 0
+        d.max_blocks = self.max_blocks if self.lane == 0 else self.side_max_blocks
         self.keep.append(d)
         self.convs.append((d, self.lane))
         flop = 2.0 * n_frames * oh * ow * pc.cout * d.cin * pc.kh * pc.kw
