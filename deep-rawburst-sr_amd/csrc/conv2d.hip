@@ -50,6 +50,8 @@ struct ConvK {
     const float* head_b;
     int head_cout;       // y is then the head's fp32 NCHW output (y_is = image stride)
     int stage_epi;       // generic kernel, MT == 4: LDS-staged 16-B-row epilogue (set by launch_conv)
+    unsigned* ctr;       // split-K arrival counters, one per (x, y) output tile (workspace head, kept zero)
+    int fin_inkernel;    // split-K: the last-arriving K slice finalizes (no conv_splitk_finalize launch)
 };
 
 template <typename T> struct Frag;
@@ -289,6 +291,38 @@ __global__ __launch_bounds__(256) void conv2d_kernel(ConvK k) {
                 *(f32x4_t*)(k.ws + ((long long)blockIdx.z * k.npix + p) * k.cw + co) = acc[i][j];
             else
                 epilogue_px<T>(k, p, co, acc[i][j], bias[i]);
+        }
+    }
+    if (k.ksplit > 1 && k.fin_inkernel) {
+        // split-K finalize without a second launch: the K slice that arrives last at this output tile's
+        // counter sums all slices' partials in slice order (bit-identical to conv_splitk_finalize) and
+        // runs the epilogue; it also resets the counter for the next launch.  Agent-scope fences publish
+        // the partials across XCDs (release before the vector atomic, acquire after it).
+        __shared__ int s_last;
+        __threadfence();
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned* ctr = k.ctr + (blockIdx.y * gridDim.x + blockIdx.x);
+            const unsigned prev = atomicAdd(ctr, 1u);
+            s_last = prev == (unsigned)(k.ksplit - 1);
+            if (s_last) atomicExch(ctr, 0u);
+        }
+        __syncthreads();
+        if (!s_last) return;
+        __threadfence();
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            const int p = p_base + j * 16 + col;
+            if (p >= k.npix) continue;
+#pragma unroll
+            for (int i = 0; i < MT; ++i) {
+                const int co = c_base + i * 16 + kgl * 4;
+                if (co >= k.cout) continue;
+                f32x4_t a = {0.f, 0.f, 0.f, 0.f};
+                for (int z = 0; z < k.ksplit; ++z)
+                    a += *(const f32x4_t*)(k.ws + ((long long)z * k.npix + p) * k.cw + co);
+                epilogue_px<T>(k, p, co, a, load_bias4(k, co));
+            }
         }
     }
 }
@@ -1056,6 +1090,18 @@ int dispatch_pipe(int cfg, const ConvK& k, const dbsr_conv_desc* d, hipStream_t 
     return launch_pipe<32, 64, 8>(k, d->n_frames, s);
 }
 
+// workspace: SPLITK_CTR_BYTES of arrival counters (zero between launches) followed by the fp32 partials
+constexpr int SPLITK_CTR_BYTES = 16384;
+// DBSR_SPLITK_INKERNEL=1: the last-arriving K slice finalizes in-kernel instead of a separate
+// conv_splitk_finalize launch.  Off by default: correct, but the agent-scope fences it needs (L2
+// write-back / invalidate per block across 8 XCDs) made the forward 46 % slower (5.02 vs 3.43 ms)
+bool splitk_inkernel_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("DBSR_SPLITK_INKERNEL");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
 bool stage_epi_enabled() {     // DBSR_STAGE_EPI=0: per-lane epilogue everywhere (A/B runs)
     static const bool on = [] {
         const char* e = getenv("DBSR_STAGE_EPI");
@@ -1070,9 +1116,11 @@ int launch_conv(const ConvK& k0, hipStream_t s) {
                   k.out_mode == DBSR_OUT_NHWC && !k.y_f32 && !k.r && k.cout % 8 == 0 && k.y_ld % 8 == 0 &&
                   k.y_c0 % 8 == 0 && k.head_cout == 0;
     dim3 grid((k.npix + 4 * NT * 16 - 1) / (4 * NT * 16), (k.cout + MT * 16 - 1) / (MT * 16), k.ksplit);
+    k.fin_inkernel = k.ksplit > 1 && splitk_inkernel_enabled() &&
+                     (long long)grid.x * grid.y * sizeof(unsigned) <= SPLITK_CTR_BYTES;
     hipLaunchKernelGGL((conv2d_kernel<T, MT, NT, XT>), grid, dim3(256), 0, s, k);
     DBSR_LAUNCH_CHECK();
-    if (k.ksplit > 1) {
+    if (k.ksplit > 1 && !k.fin_inkernel) {
         const long long n = (long long)k.npix * (k.cw / 4);
         hipLaunchKernelGGL((conv_splitk_finalize<T>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, k);
         DBSR_LAUNCH_CHECK();
@@ -1093,7 +1141,9 @@ int choose_ksplit(const ConvK& k, int mt, int nt) {
     sp = std::min(sp, 32);
     return std::max(sp, 1);
 }
-size_t splitk_bytes(const ConvK& k, int sp) { return sp > 1 ? (size_t)sp * k.npix * k.cw * sizeof(float) : 0; }
+size_t splitk_bytes(const ConvK& k, int sp) {
+    return sp > 1 ? SPLITK_CTR_BYTES + (size_t)sp * k.npix * k.cw * sizeof(float) : 0;
+}
 // generic kernel: the largest tile that still gives >= 2 blocks per CU (512 blocks); tiny PWC levels
 // (a few hundred pixels) fall through to 16 x 64-pixel tiles (and split-K) for parallelism
 int generic_min_blocks() {
@@ -1324,7 +1374,9 @@ ConvK make_convk(const dbsr_conv_desc* d) {
     k.npix = (int)((long long)d->n_frames * d->out_h * d->out_w);
     k.vec_store = (d->out_mode != DBSR_OUT_NCHW_F32) && (d->y.ld % 4 == 0) && (d->y.c0 % 4 == 0);
     k.ksplit = 1;
-    k.ws = (float*)d->workspace;
+    k.ctr = (unsigned*)d->workspace;
+    k.ws = d->workspace ? (float*)((char*)d->workspace + SPLITK_CTR_BYTES) : nullptr;
+    k.fin_inkernel = 0;
     k.cw = round_up(d->cout, 4);
     k.w_pipe = (const char*)d->w + (size_t)round_up(d->cout, 64) * k.Kp * esz;
     k.max_blocks = d->max_blocks;

@@ -122,8 +122,10 @@ int dbsr_conv2d_head(const dbsr_conv_desc* d, const float* head_w, const float* 
 int dbsr_conv_head_ok(const dbsr_conv_desc* d);
 /* Scratch bytes dbsr_conv2d would use for split-K on `d` (0 = no split).  Convs whose grid cannot fill
  * the chip split K into slices that store fp32 partials to `workspace`; a second launch sums them in
- * slice order (deterministic) and applies the epilogue.  With a smaller/NULL workspace the conv simply
- * runs unsplit.  One workspace may be shared by all convs issued on one stream. */
+ * slice order (deterministic) and applies the epilogue (DBSR_SPLITK_INKERNEL=1: the slice arriving last
+ * at an output tile does it, via per-tile arrival counters in the workspace's first 16 KiB).  The
+ * workspace must be zero-filled before its first use; every launch leaves the counters zero.  With a smaller/NULL workspace the conv simply runs
+ * unsplit.  One workspace may be shared by all convs issued on one stream. */
 size_t dbsr_conv_workspace_bytes(const dbsr_conv_desc* d);
 
 /* 81-channel cost volume of (first, second) over displacements [-4,4]^2, divided by C, followed by
