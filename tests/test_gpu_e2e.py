@@ -198,3 +198,20 @@ def test_upsample_blur_ragged_width(synth_sd):
     finally:
         DBSREngine.UPSAMPLE_BLUR = old
     assert torch.equal(res[0], res[1])
+
+
+def test_bench_shape_forward_is_deterministic(synth_sd):
+    """configs[1] shape (bf16, B=8, N=14, 48x48): the first forward of a plan and the steady-state
+    forwards (eager and HIP-graph replay) give bitwise identical offsets, predictions and weights."""
+    from dbsr_amd.burst import synthetic_bursts
+    burst, _ = synthetic_bursts(8, 14, 48, 48, sr_factor=8, seed=9)
+    burst = burst.to(DEV)
+    net = _net(synth_sd, torch.bfloat16)
+    outs = []
+    with torch.no_grad():
+        for use_graph in (False, False, True, True):
+            net.use_graph = use_graph
+            pred, aux = net(burst)
+            outs.append((pred.clone(), aux['offsets'].clone(), aux['fusion_weights'].clone()))
+    for o in outs[1:]:
+        assert all(torch.equal(a, b) for a, b in zip(o, outs[0]))
