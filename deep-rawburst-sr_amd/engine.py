@@ -71,7 +71,9 @@ class NHWC:
     """Persistent buffer of n images of h x w pixels with ld elements per pixel."""
     def __init__(self, n, h, w, ld, dtype, device):
         self.n, self.h, self.w, self.ld, self.dtype = n, h, w, ld, dtype
-        self.t = torch.zeros(n, h, w, ld, dtype=dtype, device=device)
+        g = int(os.environ.get('DBSR_GUARD_IMAGES', '0'))   # diagnostic: zero guard images after the buffer
+        self.t = torch.zeros(n + g, h, w, ld, dtype=dtype, device=device)[:n] if g else \
+            torch.zeros(n, h, w, ld, dtype=dtype, device=device)
 
     def d(self, c0=0, fmap=IDENTITY):
         return L.tensor_desc(self.t, self.ld, c0, img_stride=self.h * self.w * self.ld, fmap=fmap)
