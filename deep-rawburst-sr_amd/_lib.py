@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get('DBSR_HIP_LIB', os.path.join(_HERE, 'libdbsr_hip.so'))
 DBSR_F32, DBSR_BF16 = 0, 1
 ACT_NONE, ACT_RELU, ACT_LRELU = 0, 1, 2
 OUT_NHWC, OUT_SHUFFLE, OUT_NCHW_F32 = 0, 1, 2
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 
 class FrameMap(ctypes.Structure):
@@ -77,9 +77,6 @@ def lib():
             'dbsr_warp_bilinear': ([c_int, c_int, c_int, c_int, Tensor, c_void_p, c_ll, Tensor, c_void_p], c_int),
             'dbsr_fuse_softmax': ([c_int, c_int, c_int, c_int, Tensor, Tensor, Tensor, Tensor, Tensor, c_void_p],
                                   c_int),
-            'dbsr_warp_proj': ([c_int, c_int, c_int, Tensor, c_void_p, c_ll, Tensor, ctypes.POINTER(ConvDesc),
-                                c_void_p], c_int),
-            'dbsr_upsample_blur': ([ctypes.POINTER(ConvDesc), c_void_p, c_void_p], c_int),
             'dbsr_fuse_partial': ([c_int, c_int, c_int, c_int, c_int, Tensor, Tensor, Tensor, c_void_p, c_void_p], c_int),
             'dbsr_fuse_combine': ([c_int, c_int, c_int, c_int, c_void_p, Tensor, c_void_p], c_int),
             'dbsr_conv_transpose_k4s2': ([c_int, c_int, c_int, c_int, c_int, Tensor, c_void_p, c_void_p, Tensor,
@@ -106,7 +103,7 @@ EXPORTED = ['dbsr_abi_version', 'dbsr_last_error', 'dbsr_conv_packed_elems', 'db
             'dbsr_set_conv_algo', 'dbsr_conv_kernel_for', 'dbsr_conv_workspace_bytes', 'dbsr_conv2d_head',
             'dbsr_conv_head_ok',
             'dbsr_correlation', 'dbsr_backwarp', 'dbsr_warp_bilinear', 'dbsr_fuse_softmax',
-            'dbsr_fuse_partial', 'dbsr_fuse_combine', 'dbsr_warp_proj', 'dbsr_upsample_blur',
+            'dbsr_fuse_partial', 'dbsr_fuse_combine',
             'dbsr_conv_transpose_k4s2', 'dbsr_pack_burst', 'dbsr_flow_finalize', 'dbsr_gauss_blur3',
             'dbsr_merge_prep', 'dbsr_pwc_assemble', 'dbsr_zero']
 

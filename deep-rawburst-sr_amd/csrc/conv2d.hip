@@ -50,8 +50,6 @@ struct ConvK {
     const float* head_b;
     int head_cout;       // y is then the head's fp32 NCHW output (y_is = image stride)
     int stage_epi;       // generic kernel, MT == 4: LDS-staged 16-B-row epilogue (set by launch_conv)
-    unsigned* ctr;       // split-K arrival counters, one per (x, y) output tile (workspace head, kept zero)
-    int fin_inkernel;    // split-K: the last-arriving K slice finalizes (no conv_splitk_finalize launch)
 };
 
 template <typename T> struct Frag;
@@ -293,38 +291,6 @@ __global__ __launch_bounds__(256) void conv2d_kernel(ConvK k) {
                 epilogue_px<T>(k, p, co, acc[i][j], bias[i]);
         }
     }
-    if (k.ksplit > 1 && k.fin_inkernel) {
-        // split-K finalize without a second launch: the K slice that arrives last at this output tile's
-        // counter sums all slices' partials in slice order (bit-identical to conv_splitk_finalize) and
-        // runs the epilogue; it also resets the counter for the next launch.  Agent-scope fences publish
-        // the partials across XCDs (release before the vector atomic, acquire after it).
-        __shared__ int s_last;
-        __threadfence();
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned* ctr = k.ctr + (blockIdx.y * gridDim.x + blockIdx.x);
-            const unsigned prev = atomicAdd(ctr, 1u);
-            s_last = prev == (unsigned)(k.ksplit - 1);
-            if (s_last) atomicExch(ctr, 0u);
-        }
-        __syncthreads();
-        if (!s_last) return;
-        __threadfence();
-#pragma unroll
-        for (int j = 0; j < NT; ++j) {
-            const int p = p_base + j * 16 + col;
-            if (p >= k.npix) continue;
-#pragma unroll
-            for (int i = 0; i < MT; ++i) {
-                const int co = c_base + i * 16 + kgl * 4;
-                if (co >= k.cout) continue;
-                f32x4_t a = {0.f, 0.f, 0.f, 0.f};
-                for (int z = 0; z < k.ksplit; ++z)
-                    a += *(const f32x4_t*)(k.ws + ((long long)z * k.npix + p) * k.cw + co);
-                epilogue_px<T>(k, p, co, a, load_bias4(k, co));
-            }
-        }
-    }
 }
 
 // split-K finalize: sum the K-slice partials in slice order (deterministic), then the normal epilogue
@@ -436,6 +402,11 @@ template <typename T, int WM, int WN, int D>
 __global__ __launch_bounds__(256, 2) void conv3x3_tiled_kernel(ConvK k, int tiles_x, int tiles_y, int nct,
                                                                int nblocks) {
     using C = TileCfg<T, WM, WN, D>;
+    DBSR_OWN_SIMDS();
+    // the configurations that need more than 256 registers (accumulation registers: fp32 tiles, bf16
+    // dilation 8) run one wave per SIMD; they take the whole file too (test_capi checks every
+    // pipelined / tiled kernel's allocation)
+    if constexpr ((sizeof(T) == 4 && (WM == 64 || WN >= 64)) || (D == 8 && WN >= 64)) asm volatile("" ::: "a255");
     static_assert((C::IN_U4 + C::W_U4) * 16 <= 160 * 1024, "LDS tile exceeds 160 KiB");
     static_assert(C::NPIX * C::OSTR <= (C::IN_U4 + C::W_U4) * 16, "output staging must fit the LDS tile");
     // One LDS array (a second __shared__ object can de-pipeline LDS-DMA: cdna_hip_programming.md §5 item 4a)
@@ -738,24 +709,12 @@ struct PipeCfg {
 // each of its four 16-lane groups, the 4 lanes with equal p mod 4 read 4 distinct phys values.
 __device__ __forceinline__ int halo_phys(int p, int g) { return 2 * (g & 1) + ((g >> 1) ^ ((p >> 2) & 1)); }
 
-#ifdef DBSR_PIPE_STAMPS
-// diagnostic build only: per-block s_memtime stamps of wave 0 (tools/pipe_stamps.py)
-constexpr int STAMP_BLOCKS = 256, STAMP_N = 128;
-__device__ unsigned long long g_pipe_stamps[STAMP_BLOCKS][STAMP_N];
-#define PIPE_STAMP(idx)                                                                          \
-    do {                                                                                         \
-        if (threadIdx.x == 0 && blockIdx.x < STAMP_BLOCKS && (idx) < STAMP_N)                    \
-            g_pipe_stamps[blockIdx.x][(idx)] = __builtin_amdgcn_s_memtime();                     \
-    } while (0)
-#else
-#define PIPE_STAMP(idx) do {} while (0)
-#endif
-
 template <int WM, int TW, int TH, int EPI>
 __global__ __launch_bounds__(512, 1) void conv3x3_pipe_kernel(ConvK k, int tiles_x, int tiles_y, int nct,
                                                               int ntiles) {
     using C = PipeCfg<WM, TW, TH>;
     typedef bf16_t T;
+    DBSR_OWN_SIMDS();
     __shared__ __attribute__((aligned(16))) u32x4_t lds[C::LDS_U4];
     float* lbias = (float*)(lds + 2 * C::STAGE_U4);      // [nct * WM] fp32
 
@@ -840,11 +799,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pipe_kernel(ConvK k, int tiles
             const long long piece = ((long long)((t.cb >> 4) + blk) * nchunks + c) * 9 + tap;
             src = (const char*)((const T*)k.w_pipe + piece * 512 + lane * 8);
         }
-#ifndef DBSR_PIPE_NO_DMA
         glds16(src, lds + buf * C::STAGE_U4 + item * 64);
-#else
-        asm volatile("" ::"v"(src), "v"(buf));
-#endif
     };
 
     f32x4_t acc[WM / 16][C::GW];
@@ -931,7 +886,6 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pipe_kernel(ConvK k, int tiles
 
     int s = 0;                          // global stage index (LDS buffer = s & 1)
     Tile cur = decode(0), prev = cur;
-    PIPE_STAMP(0);
 #pragma unroll
     for (int it = 0; it < C::PER; ++it) dma(it, cur, 0, 0);
 
@@ -940,9 +894,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pipe_kernel(ConvK k, int tiles
     // residual loads (last stage) and the next stage's DMA pieces (taps 0-5).
     for (int ti = 0; ti < my_tiles; ++ti) {
         for (int c = 0; c < nchunks; ++c, ++s) {
-            PIPE_STAMP(1 + 3 * s);
             __syncthreads();            // stage s landed (vmcnt(0) + barrier); stage s-1 fully consumed
-            PIPE_STAMP(2 + 3 * s);
             const bool fin = c == 0 && ti > 0;
             if (fin) epilogue(prev);
             const bool last = c == nchunks - 1;
@@ -982,17 +934,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pipe_kernel(ConvK k, int tiles
                 }
             };
             auto mfmas = [&](const Frag<T> (&a)[WM / 16], const Frag<T> (&bq)[C::GW]) {
-#ifndef DBSR_PIPE_NO_MFMA
 #pragma unroll
                 for (int i = 0; i < WM / 16; ++i)
 #pragma unroll
                     for (int j = 0; j < C::GW; ++j) acc[i][j] = mma(a[i], bq[j], acc[i][j]);
-#else
-#pragma unroll
-                for (int i = 0; i < WM / 16; ++i) asm volatile("" ::"v"(a[i].v));
-#pragma unroll
-                for (int j = 0; j < C::GW; ++j) asm volatile("" ::"v"(bq[j].v));
-#endif
             };
             Frag<T> a0[WM / 16], b0[C::GW], a1[WM / 16], b1[C::GW];
             read_frags(0, a0, b0);
@@ -1007,7 +952,6 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pipe_kernel(ConvK k, int tiles
                     mfmas(a1, b1);
                 }
             }
-            PIPE_STAMP(3 + 3 * s);
             if (last) {
                 prev = cur;
                 cur = nxt;
@@ -1018,7 +962,6 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pipe_kernel(ConvK k, int tiles
     epilogue(prev);
 #pragma unroll
     for (int q = 0; q < C::NOUT; ++q) store_piece(q, prev);
-    PIPE_STAMP(STAMP_N - 1 > 3 * s + 1 ? 3 * s + 1 : STAMP_N - 1);
 }
 
 int g_num_cus = 0;
@@ -1090,37 +1033,16 @@ int dispatch_pipe(int cfg, const ConvK& k, const dbsr_conv_desc* d, hipStream_t 
     return launch_pipe<32, 64, 8>(k, d->n_frames, s);
 }
 
-// workspace: SPLITK_CTR_BYTES of arrival counters (zero between launches) followed by the fp32 partials
-constexpr int SPLITK_CTR_BYTES = 16384;
-// DBSR_SPLITK_INKERNEL=1: the last-arriving K slice finalizes in-kernel instead of a separate
-// conv_splitk_finalize launch.  Off by default: correct, but the agent-scope fences it needs (L2
-// write-back / invalidate per block across 8 XCDs) made the forward 46 % slower (5.02 vs 3.43 ms)
-bool splitk_inkernel_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("DBSR_SPLITK_INKERNEL");
-        return e && e[0] == '1';
-    }();
-    return on;
-}
-bool stage_epi_enabled() {     // DBSR_STAGE_EPI=0: per-lane epilogue everywhere (A/B runs)
-    static const bool on = [] {
-        const char* e = getenv("DBSR_STAGE_EPI");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
 template <typename T, int MT, int NT, typename XT = T>
 int launch_conv(const ConvK& k0, hipStream_t s) {
     ConvK k = k0;
-    k.stage_epi = MT * NT >= 2 && sizeof(T) == 2 && sizeof(XT) == 2 && stage_epi_enabled() && k.ksplit == 1 &&
+    k.stage_epi = MT * NT >= 2 && sizeof(T) == 2 && sizeof(XT) == 2 && k.ksplit == 1 &&
                   k.out_mode == DBSR_OUT_NHWC && !k.y_f32 && !k.r && k.cout % 8 == 0 && k.y_ld % 8 == 0 &&
                   k.y_c0 % 8 == 0 && k.head_cout == 0;
     dim3 grid((k.npix + 4 * NT * 16 - 1) / (4 * NT * 16), (k.cout + MT * 16 - 1) / (MT * 16), k.ksplit);
-    k.fin_inkernel = k.ksplit > 1 && splitk_inkernel_enabled() &&
-                     (long long)grid.x * grid.y * sizeof(unsigned) <= SPLITK_CTR_BYTES;
     hipLaunchKernelGGL((conv2d_kernel<T, MT, NT, XT>), grid, dim3(256), 0, s, k);
     DBSR_LAUNCH_CHECK();
-    if (k.ksplit > 1 && !k.fin_inkernel) {
+    if (k.ksplit > 1) {
         const long long n = (long long)k.npix * (k.cw / 4);
         hipLaunchKernelGGL((conv_splitk_finalize<T>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, k);
         DBSR_LAUNCH_CHECK();
@@ -1142,20 +1064,13 @@ int choose_ksplit(const ConvK& k, int mt, int nt) {
     return std::max(sp, 1);
 }
 size_t splitk_bytes(const ConvK& k, int sp) {
-    return sp > 1 ? SPLITK_CTR_BYTES + (size_t)sp * k.npix * k.cw * sizeof(float) : 0;
+    return sp > 1 ? (size_t)sp * k.npix * k.cw * sizeof(float) : 0;
 }
 // generic kernel: the largest tile that still gives >= 2 blocks per CU (512 blocks); tiny PWC levels
 // (a few hundred pixels) fall through to 16 x 64-pixel tiles (and split-K) for parallelism
-int generic_min_blocks() {
-    static const int v = [] {
-        const char* e = getenv("DBSR_GENERIC_MIN_BLOCKS");
-        return e ? std::max(1, atoi(e)) : 512;
-    }();
-    return v;
-}
 void pick_generic_tile(const ConvK& k, int& best_m, int& best_n) {
     const int mts[3] = {4, 2, 1}, nts[3] = {4, 2, 1};
-    const long long minb = generic_min_blocks();
+    const long long minb = 512;
     best_m = 1;
     best_n = 1;
     for (int a = 0; a < 3; ++a) {
@@ -1374,268 +1289,13 @@ ConvK make_convk(const dbsr_conv_desc* d) {
     k.npix = (int)((long long)d->n_frames * d->out_h * d->out_w);
     k.vec_store = (d->out_mode != DBSR_OUT_NCHW_F32) && (d->y.ld % 4 == 0) && (d->y.c0 % 4 == 0);
     k.ksplit = 1;
-    k.ctr = (unsigned*)d->workspace;
-    k.ws = d->workspace ? (float*)((char*)d->workspace + SPLITK_CTR_BYTES) : nullptr;
-    k.fin_inkernel = 0;
+    k.ws = (float*)d->workspace;
     k.cw = round_up(d->cout, 4);
     k.w_pipe = (const char*)d->w + (size_t)round_up(d->cout, 64) * k.Kp * esz;
     k.max_blocks = d->max_blocks;
     k.head_w = nullptr; k.head_b = nullptr; k.head_cout = 0;
     k.stage_epi = 0;
     return k;
-}
-
-// ------------------------------------------------------------------------------------------------
-// Warp + feature projection in one pass (encoders.py:80 then merging.py:76-78 on the warped frames):
-// the bilinear warp of a 16-pixel tile (4 waves x 4 pixels, the warp512 data flow: 16-B lanes, all
-// 16 tap loads in flight) is written to HBM (the fusion still needs it) AND to a padded LDS tile,
-// from which each wave runs the 1x1 512 -> 64 projection for 16 output channels on MFMA
-// (16 k-steps of 16x16x32 bf16; its A operand -- the wave's 16 weight rows, 64 VGPRs -- stays in
-// registers for the whole persistent loop).  Saves re-reading the warped features (P*HW*1 KiB) for
-// the projection.  Tiles are dealt in contiguous runs per XCD so a tap's neighbour rows hit the same
-// L2.  Same MFMA k-order as the generic conv on the same bf16 inputs.
-// ------------------------------------------------------------------------------------------------
-#ifndef DBSR_WARP_PROJ_PPW
-#define DBSR_WARP_PROJ_PPW 4
-#endif
-constexpr int WP_ROW = 512 + 8;   // LDS row pitch (bf16): +16 B keeps the 16 rows of a b128 read on distinct banks
-template <int PPW>
-__global__ __launch_bounds__(256, 2) void warp_proj_kernel(int n, int h, int w, dbsr_tensor feat,
-                                                           const float* __restrict__ flow, long long fis,
-                                                           dbsr_tensor out, ConvK k, int ntiles) {
-    constexpr int TP = 4 * PPW;   // pixels per tile
-    __shared__ __attribute__((aligned(16))) bf16_t tile[TP * WP_ROW];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int col = lane & 15, kgl = lane >> 4;
-    const int hw = h * w;
-    const unsigned total = (unsigned)n * hw;
-    // XCD-aware contiguous tile runs: logical block lb (grouped by XCD) owns tiles [t0, t1)
-    const unsigned b = blockIdx.x, nb = gridDim.x, xcd = b & 7, q8 = nb >> 3, r8 = nb & 7;
-    const unsigned lb = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
-    const int t0 = (int)((long long)ntiles * lb / nb), t1 = (int)((long long)ntiles * (lb + 1) / nb);
-    const bool mm = wave * 16 < k.cout;
-    Frag<bf16_t> A[16];
-    const bf16_t* wrow = (const bf16_t*)k.w + (long long)(wave * 16 + col) * k.Kp + kgl * 8;
-#pragma unroll
-    for (int ks = 0; ks < 16; ++ks) {
-        if (mm) A[ks].load(wrow + ks * 32);
-        else A[ks].zero();
-    }
-    const f32x4_t bias = load_bias4(k, wave * 16 + kgl * 4);
-    // software pipeline: the next tile's 16 tap loads per lane are in flight while this tile's
-    // projection (MFMA + epilogue) runs
-    struct Taps {
-        u32x4_t v[PPW][4];
-        float tw[PPW][4];
-        bf16_t* obase[PPW];
-        bool live[PPW];
-    };
-    auto issue = [&](int t, Taps& T) {
-#pragma unroll
-        for (int i = 0; i < PPW; ++i) {
-            const unsigned pix = (unsigned)t * TP + wave * PPW + i;
-            T.live[i] = pix < total;
-            const unsigned pc = T.live[i] ? pix : 0;
-            const int p = (int)(pc / hw), rr = (int)(pc - (unsigned)p * hw);
-            const int y = rr / w, x = rr - y * w;
-            const float* fl = flow + (long long)p * fis + rr;
-            const float gx = ((float)x + 0.5f) + fl[0];
-            const float gy = ((float)y + 0.5f) + fl[hw];
-            const float gxn = 2.0f * gx / (float)w - 1.0f, gyn = 2.0f * gy / (float)h - 1.0f;
-            const float ix = ((gxn + 1.f) * (float)w - 1.f) / 2.f;
-            const float iy = ((gyn + 1.f) * (float)h - 1.f) / 2.f;
-            const float fx0 = floorf(ix), fy0 = floorf(iy);
-            const int x0 = (int)fx0, y0 = (int)fy0;
-            const float wx1 = ix - fx0, wx0 = 1.f - wx1, wy1 = iy - fy0, wy0 = 1.f - wy1;
-            const bf16_t* fb = img_ptr<bf16_t>(feat, p) + lane * 8;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int xx = x0 + (q & 1), yy = y0 + (q >> 1);
-                const bool ok = (unsigned)xx < (unsigned)w && (unsigned)yy < (unsigned)h;
-                T.tw[i][q] = ok ? ((q & 1) ? wx1 : wx0) * ((q >> 1) ? wy1 : wy0) : 0.f;
-                T.v[i][q] = *(const u32x4_t*)(fb + (ok ? (yy * w + xx) * feat.ld : 0));
-            }
-            T.obase[i] = img_ptr<bf16_t>(out, p) + (long long)rr * out.ld + lane * 8;
-        }
-    };
-    Taps cur;
-    if (t0 < t1) issue(t0, cur);
-    for (int t = t0; t < t1; ++t) {
-        // ---- warp PPW pixels per wave ----
-#pragma unroll
-        for (int i = 0; i < PPW; ++i) {
-            f32x2_t acc[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const f32x2_t w2 = {cur.tw[i][q], cur.tw[i][q]};
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const f32x2_t x2 = {__uint_as_float(cur.v[i][q][e] << 16),
-                                        __uint_as_float(cur.v[i][q][e] & 0xffff0000u)};
-                    acc[e] = __builtin_elementwise_fma(w2, x2, acc[e]);
-                }
-            }
-            u32x4_t o;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) o[e] = pack_bf16x2(acc[e][0], acc[e][1]);
-            if (cur.live[i]) *(u32x4_t*)cur.obase[i] = o;
-            *(u32x4_t*)(tile + (wave * PPW + i) * WP_ROW + lane * 8) = o;
-        }
-        __syncthreads();
-        if (t + 1 < t1) issue(t + 1, cur);
-        // ---- 1x1 projection of the 16 warped pixels: wave -> output channels [16*wave, 16*wave+16) ----
-        if (mm) {
-#pragma unroll
-            for (int cb = 0; cb < TP / 16; ++cb) {
-                f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int ks = 0; ks < 16; ++ks) {
-                    Frag<bf16_t> B;
-                    B.v = *(const bf16x8_t*)(tile + (cb * 16 + col) * WP_ROW + ks * 32 + kgl * 8);
-                    acc = mma(A[ks], B, acc);
-                }
-                const int p = t * TP + cb * 16 + col;
-                if (p < k.npix && wave * 16 + kgl * 4 < k.cout)
-                    epilogue_px<bf16_t>(k, p, wave * 16 + kgl * 4, acc, bias);
-            }
-        }
-        __syncthreads();
-    }
-}
-
-// ------------------------------------------------------------------------------------------------
-// PixelShuffle upsampler + Gaussian blur in one kernel (upsampling.py:56-65: conv 1x1 Cin -> 64*32,
-// PixelShuffle(8), then the depthwise 3x3 Gaussian with zero padding).  Block = 8 waves over UB_TW
-// low-res pixels of one LR row y; the upsampled (bf16-rounded, exactly as the upsample kernel stores
-// it) HR tile rows 8y-1 .. 8y+8 and columns 8(x0-1) .. 8(x0+UB_TW)+7 are built in LDS -- row y's pixels
-// for all 64 sub-pixels, rows y-1 / y+1 only for the sub-row that borders the tile, LR pixels outside
-// the image as zeros (the blur's zero padding) -- then blurred from LDS with the blur kernel's tap
-// order and stored as whole 64-B pixels.  The 8*64*32*2 B per LR pixel intermediate never reaches HBM.
-// ------------------------------------------------------------------------------------------------
-constexpr int UB_TW = 8;
-constexpr int UB_COLS = (UB_TW + 2) * 8;                       // HR columns held (LR x0-1 .. x0+UB_TW)
-constexpr int UB_ROWB = UB_COLS * 64 + (UB_COLS / 8) * 16;     // bytes per HR row (16-B skew per 8 pixels)
-__device__ __forceinline__ int ub_off(int r, int c) { return r * UB_ROWB + c * 64 + (c >> 3) * 16; }
-
-struct K9f {
-    float k[9];
-};
-
-__global__ __launch_bounds__(512) void upsample_blur_kernel(ConvK k, K9f kk, int segs) {
-    __shared__ __attribute__((aligned(16))) unsigned char tile[10 * UB_ROWB];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int g = lane >> 4, col = lane & 15;
-    const int H = k.out_h, W = k.out_w;                     // low-res geometry
-    const int seg = blockIdx.x % segs;
-    const int rowid = blockIdx.x / segs;
-    const int y = rowid % H, f = rowid / H;
-    const int x0 = seg * UB_TW;
-    // pixel slots: group j (0: row y, 1: row y-1, 2: row y+1), slot col -> LR x = x0 - 1 + col
-    Frag<bf16_t> b[3][2];
-    bool valid[3];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        const int yy = j == 0 ? y : (j == 1 ? y - 1 : y + 1);
-        const int xx = x0 - 1 + col;
-        valid[j] = col < UB_TW + 2 && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
-        const bf16_t* xp = (const bf16_t*)k.x + map_frame(k.xm, f) * k.x_is +
-                           ((long long)(valid[j] ? yy : 0) * W + (valid[j] ? xx : 0)) * k.x_ld + g * 8;
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-            if (valid[j]) b[j][ks].load(xp + ks * 32);
-            else b[j][ks].zero();
-        }
-    }
-    const int m_row = 8 * (col >> 2) + (col & 3);
-    const int sx = wave;
-    // weights and bias of sub-pixel (sy, sx), prefetched one sub-row ahead (the loop is latency-bound
-    // on these L2 reads otherwise)
-    auto load_w = [&](int sy, Frag<bf16_t> (&a)[2][2], float4 (&bb)[2]) {
-        const int sub = sy * 8 + sx;
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-            for (int ks = 0; ks < 2; ++ks)
-                a[h][ks].load((const bf16_t*)k.w + (long long)(sub * 32 + m_row + 4 * h) * k.Kp + ks * 32 + g * 8);
-        if (k.bias) {
-            bb[0] = *(const float4*)(k.bias + sub * 32 + 8 * g);
-            bb[1] = *(const float4*)(k.bias + sub * 32 + 8 * g + 4);
-        } else {
-            bb[0] = make_float4(0.f, 0.f, 0.f, 0.f);
-            bb[1] = bb[0];
-        }
-    };
-    Frag<bf16_t> a_cur[2][2], a_nxt[2][2];
-    float4 bb_cur[2], bb_nxt[2];
-    load_w(0, a_cur, bb_cur);
-#pragma unroll 1
-    for (int sy = 0; sy < 8; ++sy) {
-        if (sy + 1 < 8) load_w(sy + 1, a_nxt, bb_nxt);
-        Frag<bf16_t> (&a)[2][2] = a_cur;
-        const float bv[8] = {bb_cur[0].x, bb_cur[0].y, bb_cur[0].z, bb_cur[0].w,
-                             bb_cur[1].x, bb_cur[1].y, bb_cur[1].z, bb_cur[1].w};
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            if (j == 1 && sy != 7) continue;            // row y-1: only its bottom sub-row borders the tile
-            if (j == 2 && sy != 0) continue;            // row y+1: only its top sub-row
-            f32x4_t acc[2];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                acc[h] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int ks = 0; ks < 2; ++ks) acc[h] = mma(a[h][ks], b[j][ks], acc[h]);
-            }
-            u32x4_t o = {0u, 0u, 0u, 0u};
-            if (valid[j]) {
-#pragma unroll
-                for (int e = 0; e < 2; ++e) {
-                    o[e] = pack_bf16x2(apply_act(acc[0][2 * e] + bv[2 * e], k.act),
-                                       apply_act(acc[0][2 * e + 1] + bv[2 * e + 1], k.act));
-                    o[2 + e] = pack_bf16x2(apply_act(acc[1][2 * e] + bv[4 + 2 * e], k.act),
-                                           apply_act(acc[1][2 * e + 1] + bv[4 + 2 * e + 1], k.act));
-                }
-            }
-            const int r = j == 0 ? 1 + sy : (j == 1 ? 0 : 9);
-            if (col < UB_TW + 2) *(u32x4_t*)(tile + ub_off(r, col * 8 + sx) + g * 16) = o;
-        }
-        if (sy + 1 < 8) {
-#pragma unroll
-            for (int h = 0; h < 2; ++h)
-#pragma unroll
-                for (int ks = 0; ks < 2; ++ks) a_cur[h][ks] = a_nxt[h][ks];
-            bb_cur[0] = bb_nxt[0];
-            bb_cur[1] = bb_nxt[1];
-        }
-    }
-    __syncthreads();
-    // blur: 8 HR rows x 8*UB_TW HR columns, 4 lanes (8 channels each) per HR pixel
-    const int Wh = W * 8;
-    bf16_t* ybase = (bf16_t*)k.y + map_frame(k.ym, f) * k.y_is + k.y_c0;
-#pragma unroll
-    for (int it = 0; it < 8 * 8 * UB_TW * 4 / 512; ++it) {
-        const int item = it * 512 + threadIdx.x;
-        const int px = item >> 2, q = item & 3;
-        const int pr = px / (8 * UB_TW), pc = px - pr * (8 * UB_TW);
-        const int X = x0 * 8 + pc;
-        if (X >= Wh) continue;
-        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-            for (int jj = 0; jj < 3; ++jj) {
-                const float kv = kk.k[i * 3 + jj];
-                const u32x4_t v = *(const u32x4_t*)(tile + ub_off(pr + i, 8 + pc - 1 + jj) + q * 16);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    acc[2 * e] = fmaf(kv, __uint_as_float(v[e] << 16), acc[2 * e]);
-                    acc[2 * e + 1] = fmaf(kv, __uint_as_float(v[e] & 0xffff0000u), acc[2 * e + 1]);
-                }
-            }
-        u32x4_t o;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = pack_bf16x2(acc[2 * e], acc[2 * e + 1]);
-        *(u32x4_t*)(ybase + ((long long)(y * 8 + pr) * Wh + X) * k.y_ld + q * 8) = o;
-    }
 }
 
 }  // namespace
@@ -1755,64 +1415,4 @@ extern "C" int dbsr_conv2d_head(const dbsr_conv_desc* d, const float* head_w, co
     k.head_w = head_w; k.head_b = head_b; k.head_cout = head_cout;
     k.y = head_out.ptr; k.y_f32 = 1; k.y_is = head_out.img_stride; k.y_ld = 1; k.y_c0 = 0; k.ym = head_out.map;
     return launch_pipe<32, 64, 8>(k, d->n_frames, (hipStream_t)stream);
-}
-
-#ifdef DBSR_PIPE_STAMPS
-extern "C" int dbsr_debug_pipe_stamps(unsigned long long* host, int n) {
-    const size_t bytes = std::min<size_t>((size_t)n, (size_t)STAMP_BLOCKS * STAMP_N) * sizeof(unsigned long long);
-    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pipe_stamps), bytes, 0, hipMemcpyDeviceToHost);
-}
-extern "C" int dbsr_debug_pipe_stamps_clear() {
-    static unsigned long long zeros[STAMP_BLOCKS * STAMP_N];
-    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_pipe_stamps), zeros, sizeof(zeros), 0, hipMemcpyHostToDevice);
-}
-#endif
-
-extern "C" int dbsr_warp_proj(int n, int h, int w, dbsr_tensor feat, const float* flow, long long flow_img_stride,
-                              dbsr_tensor out, const dbsr_conv_desc* d, void* stream) {
-    DBSR_CHECK_ARG(d && feat.ptr && flow && out.ptr && d->w && d->y.ptr, "warp_proj: null pointer");
-    DBSR_CHECK_ARG(feat.dtype == DBSR_BF16 && out.dtype == DBSR_BF16 && d->x.dtype == DBSR_BF16 &&
-                   d->y.dtype == DBSR_BF16, "warp_proj: bf16 only");
-    DBSR_CHECK_ARG(n > 0 && h > 0 && w > 0 && (long long)n * h * w < (1LL << 31), "warp_proj: bad sizes");
-    DBSR_CHECK_ARG(feat.ld % 8 == 0 && feat.c0 % 8 == 0 && out.ld % 8 == 0 && out.c0 % 8 == 0 &&
-                   feat.map.fpg > 0 && out.map.fpg > 0, "warp_proj: feat/out ld, c0 multiples of 8, fpg > 0");
-    // the projection must read exactly the warped tensor
-    DBSR_CHECK_ARG(d->x.ptr == out.ptr && d->x.ld == out.ld && d->x.c0 == out.c0 &&
-                   d->x.img_stride == out.img_stride && d->x.map.fpg == out.map.fpg &&
-                   d->x.map.group_stride == out.map.group_stride && d->x.map.group_offset == out.map.group_offset &&
-                   d->x.map.inner_stride == out.map.inner_stride, "warp_proj: desc->x must be the warp output");
-    DBSR_CHECK_ARG(d->n_frames == n && d->in_h == h && d->in_w == w && d->out_h == h && d->out_w == w &&
-                   d->cin == 512 && d->kh == 1 && d->kw == 1 && d->stride == 1 && d->pad == 0 && d->dil == 1 &&
-                   d->cout > 0 && d->cout <= 64 && d->cout % 4 == 0 && !d->res.ptr && !d->precise &&
-                   d->out_mode == DBSR_OUT_NHWC && d->y.map.fpg > 0 && d->y.c0 + d->cout <= d->y.ld,
-                   "warp_proj: projection must be a 1x1 512 -> <=64 NHWC conv over the warped frames");
-    ConvK k = make_convk(d);
-    DBSR_CHECK_ARG(k.Kp == 512, "warp_proj: packed K %d != 512", k.Kp);
-    constexpr int PPW = DBSR_WARP_PROJ_PPW;
-    const int ntiles = (int)(((long long)n * h * w + 4 * PPW - 1) / (4 * PPW));
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const int grid = std::min(ntiles, 2 * cus);
-    hipLaunchKernelGGL(warp_proj_kernel<PPW>, dim3(grid), dim3(256), 0, (hipStream_t)stream, n, h, w, feat, flow,
-                       flow_img_stride, out, k, ntiles);
-    DBSR_LAUNCH_CHECK();
-    return 0;
-}
-
-extern "C" int dbsr_upsample_blur(const dbsr_conv_desc* d, const float* k9, void* stream) {
-    DBSR_CHECK_ARG(d && k9 && d->x.ptr && d->w && d->y.ptr, "upsample_blur: null pointer");
-    DBSR_CHECK_ARG(d->x.ld % 8 == 0 && d->x.c0 % 8 == 0 && d->x.map.fpg > 0 && d->y.map.fpg > 0,
-                   "upsample_blur: bad input layout");
-    const ConvK k = make_convk(d);
-    DBSR_CHECK_ARG(use_upsample(d, k) && d->shuffle == 8 && k.Kp == 64 && k.cps == 32 && !d->res.ptr &&
-                   d->in_h == d->out_h && d->in_w == d->out_w && d->n_frames > 0,
-                   "upsample_blur: needs the bf16 1x1 Cin<=64 -> 64*32 PixelShuffle(8) upsampler");
-    DBSR_CHECK_ARG((long long)d->n_frames * d->out_h < (1LL << 24), "upsample_blur: too many rows");
-    K9f kk;
-    for (int i = 0; i < 9; ++i) kk.k[i] = k9[i];
-    const int segs = (d->out_w + UB_TW - 1) / UB_TW;
-    hipLaunchKernelGGL(upsample_blur_kernel, dim3((unsigned)(d->n_frames * d->out_h * segs)), dim3(512), 0,
-                       (hipStream_t)stream, k, kk, segs);
-    DBSR_LAUNCH_CHECK();
-    return 0;
 }

@@ -269,8 +269,8 @@ __global__ __launch_bounds__(256) void fuse_softmax_kernel(int B, int N, int hw,
 // twice the memory instructions).  All 2N loads are issued before the first use; the logits are
 // consumed once, so they are streamed with non-temporal loads, and the aux weights (written once,
 // never re-read by the forward) with non-temporal stores, keeping L2 for the feature rows.
-template <int NMAX, bool RECOMP>
-__global__ __launch_bounds__(256, RECOMP ? 3 : 2) void fuse512_bf16_kernel(int B, int N, int hw, dbsr_tensor logits, dbsr_tensor ref,
+template <int NMAX>
+__global__ __launch_bounds__(256, 2) void fuse512_bf16_kernel(int B, int N, int hw, dbsr_tensor logits, dbsr_tensor ref,
                                                            dbsr_tensor oth, dbsr_tensor fused, dbsr_tensor weights) {
     const unsigned pix = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
     if (pix >= (unsigned)B * hw) return;
@@ -300,9 +300,8 @@ __global__ __launch_bounds__(256, RECOMP ? 3 : 2) void fuse512_bf16_kernel(int B
             }
         }
     }
-    // RECOMP: exp() evaluated again in the weighting loop instead of keeping N x 8 fp32 values live
-    // (fewer VGPRs -> more waves per SIMD, at 2x the transcendental work)
-    float e[RECOMP ? 1 : NMAX][8], s[8];
+    // the N x 8 exp() values stay live (recomputing them at 3 waves/SIMD spilled: +65 MB scratch traffic)
+    float e[NMAX][8], s[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) s[j] = 0.f;
 #pragma unroll
@@ -317,7 +316,7 @@ __global__ __launch_bounds__(256, RECOMP ? 3 : 2) void fuse512_bf16_kernel(int B
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 s[j] += en[j];
-                if constexpr (!RECOMP) e[n][j] = en[j];
+                e[n][j] = en[j];
             }
         }
     }
@@ -331,16 +330,8 @@ __global__ __launch_bounds__(256, RECOMP ? 3 : 2) void fuse512_bf16_kernel(int B
     for (int n = 0; n < NMAX; ++n) {
         if (n < N) {
             float wn[8];
-            if constexpr (RECOMP) {
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    wn[2 * j] = __expf(__uint_as_float(lr[n][j] << 16) - m[2 * j]) * inv[2 * j];
-                    wn[2 * j + 1] = __expf(__uint_as_float(lr[n][j] & 0xffff0000u) - m[2 * j + 1]) * inv[2 * j + 1];
-                }
-            } else {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) wn[j] = e[n][j] * inv[j];
-            }
+            for (int j = 0; j < 8; ++j) wn[j] = e[n][j] * inv[j];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 acc[2 * j] = fmaf(__uint_as_float(fr[n][j] << 16), wn[2 * j], acc[2 * j]);
@@ -553,17 +544,10 @@ extern "C" int dbsr_warp_bilinear(int n, int h, int w, int c, dbsr_tensor feat, 
     return by_dtype(feat.dtype, [&](auto* tag) {
         using T = std::remove_pointer_t<decltype(tag)>;
         if (sizeof(T) == 2 && groups == 64) {
-            static const int ppw = [] {                      // DBSR_WARP_PPW (A/B): pixels per wave, 2/4/8
-                const char* e = getenv("DBSR_WARP_PPW");
-                return e ? atoi(e) : 4;
-            }();
-#define DBSR_WARP512(PPW)                                                                                      \
-    hipLaunchKernelGGL((warp512_bf16_kernel<PPW>), dim3(nblocks(((long long)n * h * w + PPW - 1) / PPW, 4)),  \
-                       dim3(256), 0, (hipStream_t)stream, n, h, w, feat, flow, flow_img_stride, out)
-            if (ppw == 2) DBSR_WARP512(2);
-            else if (ppw == 8) DBSR_WARP512(8);
-            else DBSR_WARP512(4);
-#undef DBSR_WARP512
+            // 4 pixels per wave (2: equal time, 8: occupancy-bound -- measured round 1)
+            constexpr int PPW = 4;
+            hipLaunchKernelGGL((warp512_bf16_kernel<PPW>), dim3(nblocks(((long long)n * h * w + PPW - 1) / PPW, 4)),
+                               dim3(256), 0, (hipStream_t)stream, n, h, w, feat, flow, flow_img_stride, out);
         } else if (groups % 64 == 0)
             hipLaunchKernelGGL((warp_kernel<T, true>), dim3(nblocks((long long)n * h * w * groups, 256)), dim3(256), 0,
                                (hipStream_t)stream, n, h, w, groups, feat, flow, flow_img_stride, out);
@@ -573,26 +557,6 @@ extern "C" int dbsr_warp_bilinear(int n, int h, int w, int c, dbsr_tensor feat, 
         DBSR_LAUNCH_CHECK();
         return 0;
     });
-}
-
-// DBSR_FUSE_RECOMP=1: recompute exp() in the weighting loop at 3 waves/SIMD (~2 % faster, 150 vs 153 us,
-// but its 16 spilled VGPRs add ~65 MB of scratch traffic per launch, PMC r01f); default keeps the exp()
-// values live (2 waves/SIMD, HBM traffic = the algorithmic 812 MB)
-static bool fuse_recomp() {
-    static const bool on = [] {
-        const char* e = getenv("DBSR_FUSE_RECOMP");
-        return e && e[0] == '1';
-    }();
-    return on;
-}
-
-// DBSR_FUSE512=0 selects the 4-channel kernel for A/B runs (default: the 512-channel bf16 kernel)
-static bool fuse512_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("DBSR_FUSE512");
-        return !(e && e[0] == '0');
-    }();
-    return on;
 }
 
 extern "C" int dbsr_fuse_softmax(int B, int N, int hw, int c, dbsr_tensor logits, dbsr_tensor ref, dbsr_tensor oth,
@@ -610,16 +574,12 @@ extern "C" int dbsr_fuse_softmax(int B, int N, int hw, int c, dbsr_tensor logits
         using T = std::remove_pointer_t<decltype(tag)>;
         const bool wp = groups % 64 == 0;
         if constexpr (std::is_same_v<T, bf16_t>) {
-            if (c == 512 && fuse512_enabled() && vec_ok(logits, 8) && vec_ok(ref, 8) && vec_ok(fused, 8) &&
+            if (c == 512 && vec_ok(logits, 8) && vec_ok(ref, 8) && vec_ok(fused, 8) &&
                 (N == 1 || vec_ok(oth, 8)) && (!weights.ptr || (weights.dtype == DBSR_BF16 && vec_ok(weights, 8)))) {
                 const long long waves = (long long)B * hw;
 #define DBSR_FUSE512(NM)                                                                                       \
-    if (fuse_recomp())                                                                                         \
-        hipLaunchKernelGGL((fuse512_bf16_kernel<NM, true>), dim3(nblocks(waves, 4)), dim3(256), 0,             \
-                           (hipStream_t)stream, B, N, hw, logits, ref, oth, fused, weights);                   \
-    else                                                                                                       \
-        hipLaunchKernelGGL((fuse512_bf16_kernel<NM, false>), dim3(nblocks(waves, 4)), dim3(256), 0,            \
-                           (hipStream_t)stream, B, N, hw, logits, ref, oth, fused, weights);
+    hipLaunchKernelGGL((fuse512_bf16_kernel<NM>), dim3(nblocks(waves, 4)), dim3(256), 0, (hipStream_t)stream, B, \
+                       N, hw, logits, ref, oth, fused, weights);
                 if (N <= 4) {
                     DBSR_FUSE512(4)
                 } else if (N <= 8) {

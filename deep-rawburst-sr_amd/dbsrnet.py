@@ -83,7 +83,12 @@ class DBSRNet(nn.Module):
                          accumulation is fp32 in both, flows/offsets stay fp32.
       return_fusion_weights  True: aux['fusion_weights'] is produced exactly as the reference
                          returns it (shape [B,N,C,H,W]; backed by the engine's channels-last buffer).
-      use_graph          capture the forward into a HIP graph per input shape and replay it.
+      use_graph          capture the forward into a HIP graph per input shape and replay it.  Outputs
+                         are fresh tensors (cloned from the graph's static buffers) like the reference's.
+      graph_zero_copy    with use_graph: return views of the static buffers instead (no clone); they are
+                         overwritten by the next forward of the same shape.
+      zero_flow          configs[0]'s identity-flow alignment stub (offsets = 0, no PWC-Net); changing it
+                         rebuilds the engine.
     """
     def __init__(self, encoder, merging, decoder):
         super().__init__()
@@ -94,6 +99,7 @@ class DBSRNet(nn.Module):
         self.return_fusion_weights = True
         self.use_graph = False
         self.zero_flow = False          # config 1's identity-flow alignment stub
+        self.graph_zero_copy = False
         self._engine = None
 
     def set_compute_dtype(self, dtype):

@@ -71,9 +71,7 @@ class NHWC:
     """Persistent buffer of n images of h x w pixels with ld elements per pixel."""
     def __init__(self, n, h, w, ld, dtype, device):
         self.n, self.h, self.w, self.ld, self.dtype = n, h, w, ld, dtype
-        g = int(os.environ.get('DBSR_GUARD_IMAGES', '0'))   # diagnostic: zero guard images after the buffer
-        self.t = torch.zeros(n + g, h, w, ld, dtype=dtype, device=device)[:n] if g else \
-            torch.zeros(n, h, w, ld, dtype=dtype, device=device)
+        self.t = torch.zeros(n, h, w, ld, dtype=dtype, device=device)
 
     def d(self, c0=0, fmap=IDENTITY):
         return L.tensor_desc(self.t, self.ld, c0, img_stride=self.h * self.w * self.ld, fmap=fmap)
@@ -110,12 +108,12 @@ class Plan:
     capture alike.
     """
     FORK, JOIN = '__fork__', '__join__'
-    # Two lanes (PWC-Net beside the encoder on a side stream) are OFF by default: at the bench shape
-    # (bf16, B=8) the concurrent lanes make the forward nondeterministic (offsets differ run to run by up
-    # to ~0.03, tools/check_determinism.py; the race involves the LDS-tiled/pipelined conv kernels running
-    # concurrently and is not yet found).  Single stream is deterministic.  DBSR_MULTI_STREAM=1 re-enables
-    # the lanes (~10 % faster) for investigation only.
-    MULTI_STREAM = os.environ.get('DBSR_MULTI_STREAM', '0') == '1' and os.environ.get('DBSR_SINGLE_STREAM', '0') != '1'
+    # Two lanes: PWC-Net + the offset-feature extractor on a side stream beside the frame encoder.  Safe
+    # because the LDS-DMA/MFMA conv kernels own their SIMDs (DBSR_OWN_SIMDS, csrc/common.hpp): waves of
+    # another stream's kernels sharing a CU with them computed wrong values (DESIGN.md 'two-lane race').
+    # tests/test_gpu_parity.py::test_bench_shape_two_lanes_bitwise holds the two lanes bit-identical to
+    # one stream.  DBSR_SINGLE_STREAM=1 runs everything on the caller's stream.
+    MULTI_STREAM = os.environ.get('DBSR_SINGLE_STREAM', '0') != '1'
 
     def __init__(self):
         self.ops = []        # (callable | FORK | JOIN, args, name, lane)
@@ -127,7 +125,6 @@ class Plan:
         self.lanes = {0}
         self.streams = {}
         self.max_blocks = 0  # CU cap for lane-0 persistent convs issued while a side lane runs
-        self.side_max_blocks = int(os.environ.get('DBSR_SIDE_CUS', '0'))   # same for side-lane persistent convs
 
     def add(self, name, fn, *args, work=None):
         if work is not None:
@@ -182,7 +179,7 @@ class Plan:
         d.out_mode, d.shuffle = out_mode, shuffle
         d.workspace, d.workspace_bytes = None, 0
         d.precise = 1 if precise else 0
-        d.max_blocks = self.max_blocks if self.lane == 0 else self.side_max_blocks
+        d.max_blocks = self.max_blocks if self.lane == 0 else 0
         self.keep.append(d)
         self.convs.append((d, self.lane))
         flop = 2.0 * n_frames * oh * ow * pc.cout * d.cin * pc.kh * pc.kw
@@ -208,8 +205,6 @@ class Plan:
         for lane in sorted(self.lanes):
             ds = [d for d, ln in self.convs if ln == lane]
             need = max([L.lib().dbsr_conv_workspace_bytes(d) for d in ds] + [0])
-            if os.environ.get('DBSR_NO_SPLITK', '0') == '1':
-                need = 0                      # no scratch: every conv runs unsplit
             self.ws[lane] = torch.zeros(max(need // 4, 1), dtype=torch.float32, device=device)
             for d in ds:
                 d.workspace, d.workspace_bytes = self.ws[lane].data_ptr(), need
@@ -238,29 +233,6 @@ class Plan:
             rc = fn(*args, stream)
             if rc != 0:
                 L.check(rc, name)
-
-    def segments(self):
-        """(pre, side, main, post) op lists of a plan with one fork/join: lane-0 ops before the fork, the
-        side lane's ops, lane-0 ops between fork and join, ops after the join.  None if the plan has no
-        side lane."""
-        if not any(fn is Plan.FORK for fn, _, _, _ in self.ops):
-            return None
-        segs = {'pre': [], 'side': [], 'main': [], 'post': []}
-        state = 'pre'
-        for op in self.ops:
-            fn, args, name, lane = op
-            if fn is Plan.FORK:
-                assert state == 'pre', 'one fork per plan'
-                state = 'fork'
-                continue
-            if fn is Plan.JOIN:
-                state = 'post'
-                continue
-            if state == 'fork':
-                segs['side' if lane != 0 else 'main'].append(op)
-            else:
-                segs[state].append(op)
-        return segs['pre'], segs['side'], segs['main'], segs['post']
 
     def time_ops(self, stream, reps=10):
         """Average device time (ms) of each op, each launched `reps` times back to back between two
@@ -395,51 +367,22 @@ class PWCPlanner:
 # ==================================================================================================
 # DBSR engine
 # ==================================================================================================
-def cu_mask_stream(device, cus):
-    """A HIP stream whose kernels may only run on the CUs in `cus` (hipExtStreamCreateWithCUMask), as a
-    torch ExternalStream."""
-    hip = ctypes.CDLL('libamdhip64.so')
-    n = torch.cuda.get_device_properties(device).multi_processor_count
-    words = (n + 31) // 32
-    mask = (ctypes.c_uint32 * words)()
-    for c in cus:
-        mask[c // 32] |= 1 << (c % 32)
-    sp = ctypes.c_void_p()
-    with torch.cuda.device(device):
-        rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(sp), ctypes.c_uint32(words), mask)
-    if rc != 0:
-        raise RuntimeError('hipExtStreamCreateWithCUMask failed: %d' % rc)
-    return torch.cuda.ExternalStream(sp.value, device=device)
-
-
 class DBSREngine:
-    MAIN_FIRST = os.environ.get('DBSR_MAIN_FIRST', '1') == '1'
-    LANE_GRAPHS = os.environ.get('DBSR_LANE_GRAPHS', '0') == '1'
-    # CUs reserved for the side lane (PWC-Net) while the encoder runs: the lanes then run on disjoint
-    # CU sets (hipExtStreamCreateWithCUMask) instead of contending for the same CUs; 0 = shared
-    CU_SPLIT = int(os.environ.get('DBSR_CU_SPLIT', '0'))
-    # bf16: fuse the RGB predictor into the last decoder ResBlock conv (DBSR_FUSED_HEAD=0: separate kernel)
-    FUSED_HEAD = os.environ.get('DBSR_FUSED_HEAD', '1') == '1'
-    # bf16: warp + feature projection of the warped frames in one kernel (dbsr_warp_proj).  Off by
-    # default: measured 209-215 us vs 108 + 93 us for the two kernels at cfg2 (its 64 weight VGPRs cap
-    # it at 2 waves/SIMD, half the tap loads in flight of the standalone warp); DBSR_WARP_PROJ=1 enables
-    WARP_PROJ = os.environ.get('DBSR_WARP_PROJ', '0') == '1'
-    # bf16, x8: decoder upsampler + Gaussian blur in one kernel (dbsr_upsample_blur), bitwise equal to
-    # the two kernels.  Off by default: 82 us vs 40 + 39 us -- its LDS tile (4 KiB per low-res pixel)
-    # limits a block to 8 low-res pixels, so every block re-reads the whole 256-KiB weight matrix from
-    # L2 (8x the upsampler's amortisation).  DBSR_UPSAMPLE_BLUR=1 enables it.
-    UPSAMPLE_BLUR = os.environ.get('DBSR_UPSAMPLE_BLUR', '0') == '1'
+    # bf16: fuse the RGB predictor into the last decoder ResBlock conv (False: separate fp32 kernel)
+    FUSED_HEAD = True
 
     def __init__(self, net):
         self.net = net
         self.dtype = net.compute_dtype
+        self.zero_flow = bool(getattr(net, 'zero_flow', False))   # part of every plan (no PWC-Net ops)
         self.device = None
         self.sig = None
         self.plans = {}
         self.graphs = {}
 
     def matches(self, net):
-        return net is self.net and self.dtype == net.compute_dtype and self.sig == _param_signature(net)
+        return (net is self.net and self.dtype == net.compute_dtype and self.sig == _param_signature(net)
+                and self.zero_flow == bool(getattr(net, 'zero_flow', False)))
 
     def _pack(self, device):
         net = self.net
@@ -510,29 +453,15 @@ class DBSREngine:
         rgb = NHWC(F, Hp, Wp, 8, dt, dev)
         bufs['offsets'] = torch.zeros(P, 2, H, W, dtype=torch.float32, device=dev)
         om = NHWC(F, H, W, 8, dt, dev)
-        zero_flow = getattr(self.net, 'zero_flow', False)
+        zero_flow = self.zero_flow
         plan.add('pack_burst', lib.dbsr_pack_burst, B, N, H, W, bufs['burst'].data_ptr(), raw.d(0), Hp, Wp,
                  rgb.d(0) if not zero_flow else L.NULL_TENSOR)
         # Two lanes: the alignment chain (PWC-Net -> offsets -> offset-feature extractor, many small
         # latency-bound launches) runs on a high-priority side stream beside the per-frame encoder
         # (large launches); they meet at the warp.
-        plan.fork(1, dev, priority=int(os.environ.get('DBSR_SIDE_PRIO', '-1')))
-        # while the side lane runs, lane-0 persistent convs leave CUs to it (DBSR_LANE0_CUS, 0 = all).
-        # Default: 3/4 of the CUs (192 of 256; interleaved A/B at cfg2: +1.5 % over no cap, 224 in between)
-        if not Plan.MULTI_STREAM:
-            plan_cap = 0                      # one stream: nothing runs beside the encoder
-        elif 'DBSR_LANE0_CUS' in os.environ:
-            plan_cap = int(os.environ['DBSR_LANE0_CUS'])
-        else:
-            plan_cap = torch.cuda.get_device_properties(dev).multi_processor_count * 3 // 4
-        if DBSREngine.CU_SPLIT:
-            n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
-            k = DBSREngine.CU_SPLIT
-            # every (n_cu // k)-th CU to the side lane: spread over XCDs / shader engines
-            side_cus = [c for c in range(n_cu) if c % (n_cu // k) == 0][:k]
-            main_cus = [c for c in range(n_cu) if c not in set(side_cus)]
-            plan.cu_streams = (cu_mask_stream(dev, main_cus), cu_mask_stream(dev, side_cus))
-            plan_cap = len(main_cus)
+        plan.fork(1, dev, priority=-1)
+        # while the side lane runs, lane-0 persistent convs leave a quarter of the CUs to it
+        plan_cap = torch.cuda.get_device_properties(dev).multi_processor_count * 3 // 4 if Plan.MULTI_STREAM else 0
         # ---------------- alignment (PWC-Net) ----------------
         if not zero_flow:
             flow_out = NHWC(P, Hp // 4, Wp // 4, 2, torch.float32, dev)
@@ -582,19 +511,7 @@ class DBSREngine:
             plan.add('warp', lib.dbsr_warp_bilinear, P, H, W, C, E.d(0, (N - 1, N, 1, 1)), bufs['offsets'].data_ptr(),
                      2 * H * W, Wf.d(0), work=('byte', 2.0 * P * C * H * W * es + 8.0 * P * H * W))
         if P > 0:
-            d = plan.conv('merge.proj_oth', self.proj, P, Wf, 0, hw, PJ, 0, L.ACT_RELU, ymap=(N - 1, N, 1, 1))
-            if dt == torch.bfloat16 and C == 512 and pd <= 64 and DBSREngine.WARP_PROJ:
-                # one kernel for the warp and the projection of its output (dbsr_warp_proj): replaces the
-                # two ops just emitted; reported as the 'warp' family (bytes: warp + projection output)
-                assert plan.ops[-2][2] == 'warp' and plan.ops[-1][2] == 'merge.proj_oth'
-                wbytes = plan.work[len(plan.ops) - 2][1] + 2.0 * P * H * W * pd
-                for _ in range(2):
-                    plan.ops.pop()
-                    plan.work.pop(len(plan.ops), None)
-                    plan.kernel.pop(len(plan.ops), None)
-                plan.add('warp+proj', lib.dbsr_warp_proj, P, H, W, E.d(0, (N - 1, N, 1, 1)),
-                         bufs['offsets'].data_ptr(), 2 * H * W, Wf.d(0), ctypes.byref(d), work=('byte', wbytes))
-                plan.kernel[len(plan.ops) - 1] = 'warp'
+            plan.conv('merge.proj_oth', self.proj, P, Wf, 0, hw, PJ, 0, L.ACT_RELU, ymap=(N - 1, N, 1, 1))
         plan.add('merge.prep', lib.dbsr_merge_prep, B, N, H * W, pd, PJ.d(0), WP.d(0))
         q = [NHWC(F, H, W, self.wp_init.cout, dt, dev) for _ in range(3)]
         plan.conv('merge.wp.init', self.wp_init, F, WP, 0, hw, q[0], 0, L.ACT_RELU)
@@ -641,20 +558,9 @@ class DBSREngine:
         pc = self.dec_up.cout // (S * S)
         sh = [NHWC(B, H * S, W * S, pc, dt, dev) for _ in range(3)]
         a = 0
-        if self.blur is not None and dt == torch.bfloat16 and S == 8 and DBSREngine.UPSAMPLE_BLUR:
-            # upsampler + blur in one kernel (dbsr_upsample_blur): the desc's y is the blurred output
-            kbuf = (ctypes.c_float * 9)(*self.blur)
-            plan.keep.append(kbuf)
-            d = plan.conv('dec.upsample+blur', self.dec_up, B, g[i], 0, hw, sh[1], 0, L.ACT_RELU,
-                          out_mode=L.OUT_SHUFFLE, shuffle=S)
-            fn, args, name, lane = plan.ops[-1]
-            plan.ops[-1] = (lib.dbsr_upsample_blur, (ctypes.byref(d), kbuf), name, lane)
-            plan.kernel[len(plan.ops) - 1] = 'conv1x1_shuffle'
-            a = 1
-        else:
-            plan.conv('dec.upsample', self.dec_up, B, g[i], 0, hw, sh[0], 0, L.ACT_RELU, out_mode=L.OUT_SHUFFLE,
-                      shuffle=S)
-        if self.blur is not None and a == 0:
+        plan.conv('dec.upsample', self.dec_up, B, g[i], 0, hw, sh[0], 0, L.ACT_RELU, out_mode=L.OUT_SHUFFLE,
+                  shuffle=S)
+        if self.blur is not None:
             kbuf = (ctypes.c_float * 9)(*self.blur)
             plan.keep.append(kbuf)
             plan.add('dec.blur', lib.dbsr_gauss_blur3, B, H * S, W * S, pc, sh[0].d(0), kbuf, sh[1].d(0))
@@ -677,57 +583,11 @@ class DBSREngine:
 
     @staticmethod
     def _capture(plan, dev):
-        """HIP graph(s) of a plan.  Default: one graph.  Its replay puts every kernel node on ONE hardware
-        queue (rocprofv3 trace), independent nodes without a barrier between them.  DBSR_LANE_GRAPHS=1
-        captures a plan with a side lane as four single-stream graphs instead -- pre (burst packing), side
-        (PWC-Net + offset features), main (encoder), post (after the join) -- replayed on two streams, so
-        the lanes sit on two queues; measured 1-3 % slower at cfg2 (each replay pays ~10 us of host time
-        per node, so the ~100-node side graph delays whatever is submitted after it)."""
-        segs = plan.segments() if (DBSREngine.LANE_GRAPHS or DBSREngine.CU_SPLIT) else None
-        if segs is None:
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                plan.run(L.stream_ptr(dev))
-            return g
-        if DBSREngine.CU_SPLIT:
-            main_s, side_s = plan.cu_streams
-        else:
-            main_s, side_s = torch.cuda.Stream(device=dev), plan.streams[1]
-        other = torch.cuda.Stream(device=dev)
-        out = []
-        for ops, st in zip(segs, (other, side_s, main_s, other)):
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=st):
-                plan.run_list(ops, st.cuda_stream)
-            out.append(g)
-        return tuple(out) + (main_s, side_s, torch.cuda.Event(), torch.cuda.Event(), torch.cuda.Event())
-
-    @staticmethod
-    def _replay(plan, g):
-        if not isinstance(g, tuple):
-            g.replay()
-            return
-        g_pre, g_side, g_main, g_post, main_s, side_s, ev_fork, ev_main, ev_join = g
-        cur = torch.cuda.current_stream()
-        g_pre.replay()
-        ev_fork.record(cur)
-        side_s.wait_event(ev_fork)
-        main_s.wait_event(ev_fork)
-        # Submission order matters: a replay's host cost grows with its node count (the side graph has
-        # ~100 short kernels), and the next replay call waits for it.  The main lane's few long encoder
-        # kernels are submitted first so they start at once; the side lane's kernels then stream in
-        # while the encoder runs.
-        order = [(main_s, g_main), (side_s, g_side)]
-        if not DBSREngine.MAIN_FIRST:
-            order.reverse()
-        for st, gg in order:
-            with torch.cuda.stream(st):
-                gg.replay()
-        ev_main.record(main_s)
-        ev_join.record(side_s)
-        cur.wait_event(ev_main)
-        cur.wait_event(ev_join)
-        g_post.replay()
+        """One HIP graph of the whole plan (side lanes become parallel branches of the graph)."""
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            plan.run(L.stream_ptr(dev))
+        return g
 
     def _set_fw(self, plan, want):
         fn, args, name, lane = plan.ops[plan.fuse_idx]
@@ -761,9 +621,14 @@ class DBSREngine:
                 plan.run(stream)                      # warm-up outside capture
                 g = self._capture(plan, dev)
                 self.graphs[(key, want_fw)] = g
-            self._replay(plan, g)
-            pred, offs = plan.bufs['pred'], plan.bufs['offsets']
-            fw_t = plan.FW.t
+            g.replay()
+            if getattr(self.net, 'graph_zero_copy', False):
+                # opt-in: views of the plan's static buffers, overwritten by the next forward of this shape
+                pred, offs = plan.bufs['pred'], plan.bufs['offsets']
+                fw_t = plan.FW.t if want_fw else None
+            else:
+                pred, offs = plan.bufs['pred'].clone(), plan.bufs['offsets'].clone()
+                fw_t = plan.FW.t.clone() if want_fw else None
         else:
             plan.run(stream)
             pred, offs = plan.bufs['pred'].clone(), plan.bufs['offsets'].clone()

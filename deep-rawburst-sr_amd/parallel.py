@@ -46,7 +46,12 @@ def gather_predictions(pred_local, global_batch):
 
 
 def run_sharded(net, bursts):
-    """Forward of this rank's shard of `bursts` (a global batch) and the gathered predictions."""
+    """Forward of this rank's shard of `bursts` (a global batch) and the gathered predictions.
+    Every rank validates the batch before any collective, so a too-small batch fails on all ranks
+    instead of leaving some of them blocked in the all-gather."""
+    world = dist.get_world_size()
+    if bursts.shape[0] < world:
+        raise ValueError(f'global batch {bursts.shape[0]} < world size {world}: every rank needs >= 1 burst')
     local = shard(bursts)
     pred, _ = net(local)
     return gather_predictions(pred, bursts.shape[0])

@@ -15,7 +15,6 @@
  *                             :385) incl. the leaky_relu applied by its callers, pwcnet.py:161,169
  *   dbsr_backwarp             models/alignment/pwcnet.py:16-38 (backwarp)
  *   dbsr_warp_bilinear        models/layers/warp.py:19-46 (warp), called at models/dbsr/encoders.py:80
- *   dbsr_warp_proj            the warp + merging.py:76-78 (1x1 feat_project_layer of the warped frames)
  *   dbsr_fuse_softmax         models/dbsr/merging.py:116-126 (softmax over the burst + weighted sum)
  *   dbsr_fuse_partial/combine the same softmax-fusion split over frame-sharded ranks (log-sum-exp combine)
  *   dbsr_conv2d               nn.Conv2d (+ReLU/LeakyReLU, ResBlock residual, PixelShuffle epilogue)
@@ -26,7 +25,6 @@
  *   dbsr_flow_finalize        pwcnet.py:274-279 (x20 bilinear upsample + rescale) + merging.py:98-105
  *                             (offsets_all = cat(0, offsets) % offset_modulo)
  *   dbsr_gauss_blur3          upsampling.py:59-65 (depthwise Gaussian, zero padding)
- *   dbsr_upsample_blur        upsampling.py:56-65 (PixelShuffle upsampler + Gaussian blur, one pass)
  *   dbsr_merge_prep           merging.py:79-89 (base_feat_proj, feat_diff_proj)
  *   dbsr_pwc_assemble         pwcnet.py:171 (cat([tenVolume, tenFirst, tenFlow, tenFeat]))
  */
@@ -40,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DBSR_ABI_VERSION 6
+#define DBSR_ABI_VERSION 7
 
 enum { DBSR_F32 = 0, DBSR_BF16 = 1 };
 enum { DBSR_ACT_NONE = 0, DBSR_ACT_RELU = 1, DBSR_ACT_LRELU = 2 };      /* LeakyReLU slope 0.1 */
@@ -122,10 +120,8 @@ int dbsr_conv2d_head(const dbsr_conv_desc* d, const float* head_w, const float* 
 int dbsr_conv_head_ok(const dbsr_conv_desc* d);
 /* Scratch bytes dbsr_conv2d would use for split-K on `d` (0 = no split).  Convs whose grid cannot fill
  * the chip split K into slices that store fp32 partials to `workspace`; a second launch sums them in
- * slice order (deterministic) and applies the epilogue (DBSR_SPLITK_INKERNEL=1: the slice arriving last
- * at an output tile does it, via per-tile arrival counters in the workspace's first 16 KiB).  The
- * workspace must be zero-filled before its first use; every launch leaves the counters zero.  With a smaller/NULL workspace the conv simply runs
- * unsplit.  One workspace may be shared by all convs issued on one stream. */
+ * slice order (deterministic) and applies the epilogue.  With a smaller/NULL workspace the conv simply
+ * runs unsplit.  One workspace may be shared by all convs issued on one stream. */
 size_t dbsr_conv_workspace_bytes(const dbsr_conv_desc* d);
 
 /* 81-channel cost volume of (first, second) over displacements [-4,4]^2, divided by C, followed by
@@ -143,24 +139,11 @@ int dbsr_backwarp(int n, int h, int w, int c, dbsr_tensor in, dbsr_tensor flow, 
 int dbsr_warp_bilinear(int n, int h, int w, int c, dbsr_tensor feat, const float* flow,
                        long long flow_img_stride, dbsr_tensor out, void* stream);
 
-/* dbsr_warp_bilinear (bf16, 512 channels) fused with the 1x1 feature projection that consumes its
- * output (merging.py:76-78, feat_project_layer on the warped frames): out receives the warped
- * features exactly as dbsr_warp_bilinear writes them, and d (a 1x1 cin=512 -> cout<=64 NHWC conv
- * whose x is `out`, bias/act as usual, no residual) is applied to them in the same pass. */
-int dbsr_warp_proj(int n, int h, int w, dbsr_tensor feat, const float* flow, long long flow_img_stride,
-                   dbsr_tensor out, const dbsr_conv_desc* d, void* stream);
-
 /* Softmax over the burst of logits[b,n] and weighted sum of feats[b,n].  Frame (b,n): logits image
  * b*N+n; feature image: n==0 -> ref (map applied to b), n>0 -> oth (map applied to b*(N-1)+n-1).
  * weights (optional, ptr NULL to skip): NHWC images b*N+n.  fused: NHWC images b. */
 int dbsr_fuse_softmax(int B, int N, int hw, int c, dbsr_tensor logits, dbsr_tensor ref, dbsr_tensor oth,
                       dbsr_tensor fused, dbsr_tensor weights, void* stream);
-
-/* The decoder's PixelShuffle upsampler and Gaussian blur in one pass (upsampling.py:56-65): d is the
- * bf16 1x1 conv (cin <= 64, cout = 64*32, shuffle 8, DBSR_OUT_SHUFFLE, packed with shuffle = 8) whose
- * y is the BLURRED output; k9: the 3x3 kernel (host memory, row-major).  Equals dbsr_conv2d(d) into a
- * temporary followed by dbsr_gauss_blur3 (same bf16 rounding of the intermediate). */
-int dbsr_upsample_blur(const dbsr_conv_desc* d, const float* k9, void* stream);
 
 /* Frame-sharded fusion (the softmax over the burst of models/dbsr/merging.py:116-124
  * split over ranks holding disjoint frame subsets).  dbsr_fuse_partial: statistics of the local frames

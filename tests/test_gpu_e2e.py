@@ -132,74 +132,6 @@ def test_frame_sharded_fusion_hip(golden, synth_sd, world):
     np.testing.assert_allclose(pred.double().sum(dim=(-2, -1)).numpy(), g['pred_sum'], rtol=1e-4)
 
 
-def test_warp_proj_fused_matches_two_kernels(golden, synth_sd):
-    """dbsr_warp_proj (warp + 1x1 projection in one kernel) against dbsr_warp_bilinear followed by the
-    generic 1x1 conv: same bf16 inputs, same MFMA k-order -> bitwise identical forward."""
-    from dbsr_amd.engine import DBSREngine
-    g = golden('e2e_b1n14')
-    burst = torch.from_numpy(g['burst']).to(DEV)
-    outs = []
-    old = DBSREngine.WARP_PROJ
-    try:
-        for flag in (True, False):
-            DBSREngine.WARP_PROJ = flag
-            net = _net(synth_sd, torch.bfloat16)
-            with torch.no_grad():
-                pred, aux = net(burst)
-            names = [op[2] for op in net._engine.plans[tuple(burst.shape[i] for i in (0, 1, 3, 4))].ops]
-            assert ('warp+proj' in names) == flag
-            outs.append((pred.clone(), aux['fusion_weights'].clone()))
-    finally:
-        DBSREngine.WARP_PROJ = old
-    assert torch.equal(outs[0][0], outs[1][0])
-    assert torch.equal(outs[0][1], outs[1][1])
-
-
-def test_upsample_blur_fused_matches_two_kernels(golden, synth_sd):
-    """dbsr_upsample_blur (upsampler + Gaussian blur in one pass, intermediate in LDS) against the
-    upsampler kernel followed by dbsr_gauss_blur3: same bf16 rounding, same tap order -> bitwise equal."""
-    from dbsr_amd.engine import DBSREngine
-    outs = []
-    old = DBSREngine.UPSAMPLE_BLUR
-    for name in ('e2e_b1n4', 'e2e_b1n3_h40w56'):       # 40x56: a partial last column segment (56 % 8 = 0, 40 rows)
-        g = golden(name)
-        burst = torch.from_numpy(g['burst']).to(DEV)
-        res = []
-        try:
-            for flag in (True, False):
-                DBSREngine.UPSAMPLE_BLUR = flag
-                net = _net(synth_sd, torch.bfloat16)
-                with torch.no_grad():
-                    pred, _ = net(burst)
-                key = tuple(burst.shape[i] for i in (0, 1, 3, 4))
-                names = [op[2] for op in net._engine.plans[key].ops]
-                assert ('dec.upsample+blur' in names) == flag
-                res.append(pred.clone())
-        finally:
-            DBSREngine.UPSAMPLE_BLUR = old
-        assert torch.equal(res[0], res[1]), name
-
-
-def test_upsample_blur_ragged_width(synth_sd):
-    """Low-res width not a multiple of the kernel's 8-pixel segment (zero-padded halo at the right edge)."""
-    from dbsr_amd.engine import DBSREngine
-    from dbsr_amd.burst import synthetic_bursts
-    burst, _ = synthetic_bursts(2, 3, 20, 36, sr_factor=8, seed=5)
-    burst = burst.to(DEV)
-    old = DBSREngine.UPSAMPLE_BLUR
-    res = []
-    try:
-        for flag in (True, False):
-            DBSREngine.UPSAMPLE_BLUR = flag
-            net = _net(synth_sd, torch.bfloat16)
-            with torch.no_grad():
-                pred, _ = net(burst)
-            res.append(pred.clone())
-    finally:
-        DBSREngine.UPSAMPLE_BLUR = old
-    assert torch.equal(res[0], res[1])
-
-
 def test_bench_shape_forward_is_deterministic(synth_sd):
     """configs[1] shape (bf16, B=8, N=14, 48x48): the first forward of a plan and the steady-state
     forwards (eager and HIP-graph replay) give bitwise identical offsets, predictions and weights."""

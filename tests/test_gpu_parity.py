@@ -1,0 +1,169 @@
+"""Parity at the benchmarked workloads (BASELINE.json configs[1], configs[2]) against the oracle run
+in-test on the same seeded bursts, and element-wise checks of the pipelined conv kernel's compile-time
+epilogues (the variants the bench-shape forward dispatches).
+
+Tolerances (north_star: fp32 <= 1e-3 max-abs; bf16: PSNR within 0.01 dB of the reference):
+  * configs[1] (bf16, B=8): per-burst |PSNR - PSNR_ref| <= 0.01 dB against the synthetic ground truth
+    with compute_score's 2^14 quantisation and boundary_ignore=40; offsets max-abs <= OFFS_TOL px
+    (bf16 PWC-Net features, fp32 flow accumulation); quantised pred: 99.9 % of values within
+    PRED_Q_TOL quanta of the oracle's and none beyond PRED_Q_MAX (bf16 activations through ~70 convs
+    with seeded random weights; measured on MI355X: p99.9 234, max 463 quanta, PSNR delta 0.0047 dB,
+    offsets 0.013 px).
+  * configs[2] (fp32, B=4, 80x80): pred and offsets max-abs <= 1e-3.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+OFFS_TOL = 0.05
+PRED_Q_TOL = 320          # 320 of 2^14 quanta = 0.0195 in [0, 1]
+PRED_Q_MAX = 800          # 0.049
+
+
+def _net(synth_sd, dtype):
+    import dbsr_amd
+    net = dbsr_amd.dbsrnet_cvpr2021(**dbsr_amd.DBSR_SYNTHETIC_KWARGS)
+    net.load_state_dict(synth_sd)
+    return net.to(DEV).eval().set_compute_dtype(dtype)
+
+
+def _psnr_q(pred, gt, bi=40):
+    """compute_score.py:110-115 quantisation + PSNR(boundary_ignore=40) (image_quality_v2.py:69-101)."""
+    q = (pred.clamp(0.0, 1.0) * 2 ** 14).short().float() / 2 ** 14
+    return [float(10 * torch.log10(1.0 / ((p - g_)[..., bi:-bi, bi:-bi] ** 2).mean())) for p, g_ in zip(q, gt)]
+
+
+@pytest.fixture(scope='module')
+def bench_case(synth_sd):
+    """configs[1] inputs and the oracle's fp32 forward of them (computed once per module)."""
+    from dbsr_amd.burst import synthetic_bursts
+    from oracle import dbsr_oracle as orc
+    burst, gt = synthetic_bursts(8, 14, 48, 48, sr_factor=8, seed=101)
+    with torch.no_grad():
+        ref, raux = orc.dbsr_forward(burst, synth_sd)
+    return burst, gt, ref, raux['offsets']
+
+
+def _check_bench(pred, offs, bench_case):
+    burst, gt, ref, roffs = bench_case
+    pred, offs = pred.float().cpu(), offs.cpu()
+    od = (offs - roffs).abs().max().item()
+    q = (pred.clamp(0, 1) * 2 ** 14).short().int()
+    rq = (ref.clamp(0, 1) * 2 ** 14).short().int()
+    qd = (q - rq).abs().float()
+    mine, theirs = _psnr_q(pred, gt), _psnr_q(ref, gt)
+    dpsnr = max(abs(a - b) for a, b in zip(mine, theirs))
+    print('offsets max-abs %.4g  pred quanta max %d p99.9 %.1f mean %.2f  PSNR delta max %.5f dB' % (
+        od, int(qd.max()), float(torch.quantile(qd.flatten()[::7], 0.999)), float(qd.mean()), dpsnr))
+    assert od <= OFFS_TOL
+    assert float((qd > PRED_Q_TOL).float().mean()) <= 1e-3
+    assert float(qd.max()) <= PRED_Q_MAX
+    assert dpsnr <= 0.01
+
+
+def test_bench_shape_bf16_vs_oracle(synth_sd, bench_case):
+    """configs[1] exactly as bench.py runs it (bf16, B=8, N=14, 48x48, HIP-graph replay, default kernel
+    dispatch -- the pipelined 3x3 kernel for every trunk conv) against the oracle."""
+    net = _net(synth_sd, torch.bfloat16)
+    net.use_graph = True
+    with torch.no_grad():
+        net(bench_case[0].to(DEV))                 # capture
+        pred, aux = net(bench_case[0].to(DEV))     # replay
+    _check_bench(pred, aux['offsets'], bench_case)
+
+
+def test_bench_shape_two_lanes_bitwise(synth_sd, bench_case):
+    """PWC-Net on a side stream beside the encoder (two lanes, eager and graph) gives bit-identical
+    results to the single-stream forward at the bench shape, over repeated forwards."""
+    from dbsr_amd import engine
+    burst = bench_case[0].to(DEV)
+    outs = {}
+    old = engine.Plan.MULTI_STREAM
+    try:
+        for multi in (False, True):
+            engine.Plan.MULTI_STREAM = multi
+            net = _net(synth_sd, torch.bfloat16)
+            res = []
+            with torch.no_grad():
+                for use_graph in (False, False, False, True, True, True):
+                    net.use_graph = use_graph
+                    pred, aux = net(burst)
+                    res.append((pred, aux['offsets'], aux['fusion_weights']))
+            outs[multi] = res
+    finally:
+        engine.Plan.MULTI_STREAM = old
+    ref = outs[False][0]
+    for multi in (False, True):
+        for i, o in enumerate(outs[multi]):
+            for a, b, name in zip(o, ref, ('pred', 'offsets', 'fusion_weights')):
+                assert torch.equal(a, b), (multi, i, name, (a.float() - b.float()).abs().max().item())
+
+
+def test_cfg3_batch4_fp32_vs_oracle(synth_sd):
+    """configs[2] at its stated batch (BurstSR real crops: B=4, 14 frames, 80x80, fp32; 1/1023 RAW
+    quantisation) against the oracle: max-abs <= 1e-3 on pred and offsets."""
+    from dbsr_amd.burst import synthetic_bursts
+    from oracle import dbsr_oracle as orc
+    burst, _ = synthetic_bursts(4, 14, 80, 80, sr_factor=8, seed=13)
+    burst = (burst * 1023).round() / 1023
+    net = _net(synth_sd, torch.float32)
+    with torch.no_grad():
+        pred, aux = net(burst.to(DEV))
+        ref, raux = orc.dbsr_forward(burst, synth_sd)
+    assert pred.shape == (4, 3, 640, 640)
+    assert (aux['offsets'].cpu() - raux['offsets']).abs().max().item() <= 1e-3
+    assert (pred.cpu() - ref).abs().max().item() <= 1e-3
+
+
+# (act, residual, post_act, cin, cout): the pipelined kernel's compile-time epilogues at the widths the
+# forward uses -- EPI 1 act(ReLU) no residual (encoder init-out, ResBlock conv1, wp.init),
+# EPI 2 no act + residual + ReLU (ResBlock conv2), EPI 3 plain (wp.out 128 -> 512)
+PIPE_EPI = [
+    (1, False, 0, 64, 64), (1, False, 0, 64, 512), (1, False, 0, 192, 128),
+    (0, True, 1, 64, 64), (0, True, 1, 128, 128), (0, True, 1, 32, 32),
+    (0, False, 0, 128, 512), (0, False, 0, 64, 64), (1, False, 0, 32, 32),
+]
+
+
+@pytest.mark.parametrize('case', PIPE_EPI)
+def test_pipe_epilogue_variants(ops_mod, case):
+    from dbsr_amd import _lib
+    act, use_res, post, cin, cout = case
+    H, W = (8, 96) if cout > 32 else (8, 128)
+    N = 2
+    gen = torch.Generator().manual_seed(cin * 13 + cout + act * 7 + post)
+    x = torch.randn(N, cin, H, W, generator=gen)
+    w = torch.randn(cout, cin, 3, 3, generator=gen) / (cin * 9) ** 0.5
+    b = torch.randn(cout, generator=gen) * 0.1
+    res = torch.randn(N, cout, H, W, generator=gen) if use_res else None
+    xb, wb = x.to(torch.bfloat16).float(), w.to(torch.bfloat16).float()
+    ref = F.conv2d(xb, wb, b, padding=1)
+    if act:
+        ref = F.relu(ref)
+    if use_res:
+        # the kernel adds the residual to the fp32 conv value and rounds once
+        ref = ref + res.to(torch.bfloat16).float()
+    if post:
+        ref = F.relu(ref)
+    outs = {}
+    try:
+        for algo in (3, 0):
+            _lib.lib().dbsr_set_conv_algo(algo)
+            outs[algo] = ops_mod.conv2d(x.to(DEV), w.to(DEV), b.to(DEV), padding=1, act=act,
+                                        residual=res.to(DEV) if use_res else None, post_act=post,
+                                        compute_dtype=torch.bfloat16).float().cpu()
+    finally:
+        _lib.lib().dbsr_set_conv_algo(2)
+    # bf16 output: one rounding of the fp32 result (2^-8 relative)
+    np.testing.assert_allclose(outs[3].numpy(), ref.numpy(), atol=2e-2, rtol=1e-2)
+    np.testing.assert_allclose(outs[3].numpy(), outs[0].numpy(), atol=2e-2, rtol=1e-2)
+    assert (outs[3] - ref).abs().mean() < 2e-3
+
+
+@pytest.fixture(scope='module')
+def ops_mod():
+    from dbsr_amd import ops as O
+    return O
