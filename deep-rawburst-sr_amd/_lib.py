@@ -41,7 +41,7 @@ class ConvDesc(ctypes.Structure):
                 ('res', Tensor), ('post_act', ctypes.c_int),
                 ('out_mode', ctypes.c_int), ('shuffle', ctypes.c_int),
                 ('workspace', ctypes.c_void_p), ('workspace_bytes', ctypes.c_size_t), ('precise', ctypes.c_int),
-                ('max_blocks', ctypes.c_int)]
+                ('max_blocks', ctypes.c_int), ('gate', Tensor)]
 
 
 _lib = None
@@ -88,6 +88,23 @@ def lib():
             'dbsr_merge_prep': ([c_int, c_int, c_int, c_int, Tensor, Tensor, c_void_p], c_int),
             'dbsr_pwc_assemble': ([c_int, c_int, c_int, c_int, Tensor, Tensor, Tensor, Tensor, c_void_p], c_int),
             'dbsr_zero': ([c_void_p, c_size_t, c_void_p], c_int),
+            'dbsr_conv_wgrad_workspace_bytes': ([c_int, c_int, c_int, c_int, c_int, c_int], c_size_t),
+            'dbsr_conv_wgrad': ([c_int, c_int, c_int, Tensor, c_int, Tensor, c_int, c_int, c_void_p, c_int, c_void_p,
+                                 c_size_t, c_void_p], c_int),
+            'dbsr_chan_sum_workspace_bytes': ([c_int, c_int, c_int], c_size_t),
+            'dbsr_chan_sum': ([c_int, c_int, c_int, Tensor, c_void_p, c_int, c_void_p, c_size_t, c_void_p], c_int),
+            'dbsr_l1_loss_backward': ([c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, Tensor, c_void_p,
+                                       c_void_p, c_size_t, c_void_p], c_int),
+            'dbsr_unshuffle_gate': ([c_int, c_int, c_int, c_int, c_int, Tensor, Tensor, Tensor, c_void_p], c_int),
+            'dbsr_fuse_backward': ([c_int, c_int, c_int, c_int, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor,
+                                    Tensor, c_void_p], c_int),
+            'dbsr_merge_prep_backward': ([c_int, c_int, c_int, c_int, Tensor, Tensor, Tensor, c_void_p], c_int),
+            'dbsr_warp_backward': ([c_int, c_int, c_int, c_int, Tensor, c_void_p, c_ll, c_void_p, FrameMap, c_ll,
+                                    c_void_p], c_int),
+            'dbsr_enc_grad_gate': ([c_int, c_int, c_int, c_int, Tensor, c_void_p, Tensor, Tensor, c_void_p], c_int),
+            'dbsr_adam_step': ([c_ll, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_float, c_float, c_float, c_int,
+                                c_float, c_void_p], c_int),
+            'dbsr_dgrad_weights': ([c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p], c_int),
         }
         for name, (args, res) in sigs.items():
             fn = getattr(L, name)
@@ -105,7 +122,10 @@ EXPORTED = ['dbsr_abi_version', 'dbsr_last_error', 'dbsr_conv_packed_elems', 'db
             'dbsr_correlation', 'dbsr_backwarp', 'dbsr_warp_bilinear', 'dbsr_fuse_softmax',
             'dbsr_fuse_partial', 'dbsr_fuse_combine',
             'dbsr_conv_transpose_k4s2', 'dbsr_pack_burst', 'dbsr_flow_finalize', 'dbsr_gauss_blur3',
-            'dbsr_merge_prep', 'dbsr_pwc_assemble', 'dbsr_zero']
+            'dbsr_merge_prep', 'dbsr_pwc_assemble', 'dbsr_zero', 'dbsr_conv_wgrad_workspace_bytes', 'dbsr_conv_wgrad',
+            'dbsr_chan_sum_workspace_bytes', 'dbsr_chan_sum', 'dbsr_l1_loss_backward', 'dbsr_unshuffle_gate',
+            'dbsr_fuse_backward', 'dbsr_merge_prep_backward', 'dbsr_warp_backward', 'dbsr_enc_grad_gate',
+            'dbsr_adam_step', 'dbsr_dgrad_weights']
 
 
 def check(rc, what):

@@ -38,6 +38,7 @@ struct ConvK {
     void* y; int y_f32; long long y_is; int y_ld, y_c0; dbsr_frame_map ym; int out_h, out_w;
     int act;
     const void* r; long long r_is; int r_ld, r_c0; dbsr_frame_map rm; int post_act;
+    const void* gt; long long g_is; int g_ld, g_c0; dbsr_frame_map gm;   // gate (ReLU backward): out *= (gate > 0)
     int out_mode, shuffle, cps;
     int npix;
     int vec_store;
@@ -147,6 +148,13 @@ __device__ __forceinline__ void epilogue_px(const ConvK& k, int p, int co, const
             } else {
                 const T* rp = (const T*)k.r + roff;
                 for (int r = 0; r < nvalid; ++r) v[r] = apply_act(v[r] + elem<T>::ld(rp + r), k.post_act);
+            }
+        }
+        if (k.gt) {
+            const long long goff = map_frame(k.gm, f) * k.g_is + (long long)rr * k.g_ld + k.g_c0 + co;
+            for (int r = 0; r < nvalid; ++r) {
+                const float gv = k.y_f32 ? ((const float*)k.gt)[goff + r] : elem<T>::ld((const T*)k.gt + goff + r);
+                v[r] = gv > 0.f ? v[r] : 0.f;
             }
         }
         store4<T>(k, map_frame(k.ym, f) * k.y_is + (long long)rr * k.y_ld + k.y_c0 + co, v, nvalid);
@@ -545,7 +553,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_tiled_kernel(ConvK k, int tile
 
     // ---- epilogue: bias + act into an LDS [pixel][cout] tile, then whole 16-B rows per lane ----
     const bool staged = !k.y_f32 && k.y_ld % 8 == 0 && k.y_c0 % 8 == 0 && k.cout % 8 == 0 &&
-                        (!k.r || (k.r_ld % 8 == 0 && k.r_c0 % 8 == 0));
+                        (!k.r || (k.r_ld % 8 == 0 && k.r_c0 % 8 == 0)) && (!k.gt || (k.g_ld % 8 == 0 && k.g_c0 % 8 == 0));
     if (staged) {
         char* ob = (char*)lds;
 #pragma unroll
@@ -574,6 +582,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_tiled_kernel(ConvK k, int tile
         constexpr int PER = (NCH + 255) / 256;
         const int cvalid = min(WM, k.cout - c_base);
         const T* rbase = k.r ? (const T*)k.r + map_frame(k.rm, f) * k.r_is + k.r_c0 + c_base : nullptr;
+        const T* gbase = k.gt ? (const T*)k.gt + map_frame(k.gm, f) * k.g_is + k.g_c0 + c_base : nullptr;
         T* ybase = (T*)k.y + map_frame(k.ym, f) * k.y_is + k.y_c0 + c_base;
         u32x4_t rv[PER];
         long long off[PER];
@@ -614,6 +623,20 @@ __global__ __launch_bounds__(256, 2) void conv3x3_tiled_kernel(ConvK k, int tile
                                                            k.post_act));
                 }
             }
+            if (gbase) {
+                const u32x4_t gv = *(const u32x4_t*)(gbase + off[e] * k.g_ld + sc * EPC);
+                if constexpr (sizeof(T) == 2) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const unsigned keep = (__uint_as_float(gv[q] << 16) > 0.f ? 0x0000ffffu : 0u) |
+                                              (__uint_as_float(gv[q] & 0xffff0000u) > 0.f ? 0xffff0000u : 0u);
+                        val[q] &= keep;
+                    }
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) val[q] = __uint_as_float(gv[q]) > 0.f ? val[q] : 0u;
+                }
+            }
             *(u32x4_t*)(ybase + off[e] * k.y_ld + sc * EPC) = val;
         }
         return;
@@ -637,6 +660,13 @@ __global__ __launch_bounds__(256, 2) void conv3x3_tiled_kernel(ConvK k, int tile
                 for (int r = 0; r < nvalid; ++r)
                     v[r] = apply_act(v[r] + (k.y_f32 ? ((const float*)k.r)[roff + r] : elem<T>::ld((const T*)k.r + roff + r)),
                                      k.post_act);
+            }
+            if (k.gt) {
+                const long long goff = map_frame(k.gm, f) * k.g_is + (long long)rr * k.g_ld + k.g_c0 + co;
+                for (int r = 0; r < nvalid; ++r) {
+                    const float gv = k.y_f32 ? ((const float*)k.gt)[goff + r] : elem<T>::ld((const T*)k.gt + goff + r);
+                    v[r] = gv > 0.f ? v[r] : 0.f;
+                }
             }
             store4<T>(k, map_frame(k.ym, f) * k.y_is + (long long)rr * k.y_ld + k.y_c0 + co, v, nvalid);
         }
@@ -1019,6 +1049,7 @@ int pick_pipe(const dbsr_conv_desc* d) {
         d->pad != 1 || d->dil != 1 || d->cin <= 16 || d->out_mode != DBSR_OUT_NHWC || d->y.dtype != DBSR_BF16)
         return 0;
     if (d->y.ld % 8 || d->y.c0 % 8 || d->cout % 8 || (d->res.ptr && (d->res.ld % 8 || d->res.c0 % 8))) return 0;
+    if (d->gate.ptr) return 0;                                   // gated (backward) convs: tiled/generic kernels
     if (cin_pad(d->cin) * 2 + 64 > ZERO_PAGE_BYTES || d->cout > 512) return 0;
     int cfg = 0, tw = 0, wm = 0;
     if (d->cout > 32 && d->out_w % 48 == 0) { cfg = 1; tw = 48; wm = 64; }
@@ -1037,7 +1068,7 @@ template <typename T, int MT, int NT, typename XT = T>
 int launch_conv(const ConvK& k0, hipStream_t s) {
     ConvK k = k0;
     k.stage_epi = MT * NT >= 2 && sizeof(T) == 2 && sizeof(XT) == 2 && k.ksplit == 1 &&
-                  k.out_mode == DBSR_OUT_NHWC && !k.y_f32 && !k.r && k.cout % 8 == 0 && k.y_ld % 8 == 0 &&
+                  k.out_mode == DBSR_OUT_NHWC && !k.y_f32 && !k.r && !k.gt && k.cout % 8 == 0 && k.y_ld % 8 == 0 &&
                   k.y_c0 % 8 == 0 && k.head_cout == 0;
     dim3 grid((k.npix + 4 * NT * 16 - 1) / (4 * NT * 16), (k.cout + MT * 16 - 1) / (MT * 16), k.ksplit);
     hipLaunchKernelGGL((conv2d_kernel<T, MT, NT, XT>), grid, dim3(256), 0, s, k);
@@ -1252,7 +1283,7 @@ __global__ __launch_bounds__(512) void upsample_shuffle_kernel(ConvK k) {
 }
 
 bool use_upsample(const dbsr_conv_desc* d, const ConvK& k) {
-    return d->x.dtype == DBSR_BF16 && d->y.dtype == DBSR_BF16 && !d->precise && d->out_mode == DBSR_OUT_SHUFFLE &&
+    return d->x.dtype == DBSR_BF16 && d->y.dtype == DBSR_BF16 && !d->precise && d->out_mode == DBSR_OUT_SHUFFLE && !d->gate.ptr &&
            d->kh == 1 && d->kw == 1 && d->stride == 1 && d->pad == 0 && k.cps == 32 &&
            (d->shuffle * d->shuffle) % 8 == 0 && k.Kp % 32 == 0 && k.Kp <= 128 && d->y.ld % 8 == 0 &&
            d->y.c0 % 8 == 0 && g_tiled_enabled;
@@ -1284,6 +1315,8 @@ ConvK make_convk(const dbsr_conv_desc* d) {
     k.ym = d->y.map; k.out_h = d->out_h; k.out_w = d->out_w; k.act = d->act;
     k.r = d->res.ptr; k.r_is = d->res.img_stride; k.r_ld = d->res.ld; k.r_c0 = d->res.c0; k.rm = d->res.map;
     if (!k.r) k.rm = d->y.map;
+    k.gt = d->gate.ptr; k.g_is = d->gate.img_stride; k.g_ld = d->gate.ld; k.g_c0 = d->gate.c0; k.gm = d->gate.map;
+    if (!k.gt) k.gm = d->y.map;
     k.post_act = d->post_act; k.out_mode = d->out_mode; k.shuffle = d->shuffle;
     k.cps = d->out_mode == DBSR_OUT_SHUFFLE ? d->cout / (d->shuffle * d->shuffle) : 0;
     k.npix = (int)((long long)d->n_frames * d->out_h * d->out_w);
@@ -1384,6 +1417,9 @@ extern "C" int dbsr_conv2d(const dbsr_conv_desc* d, void* stream) {
     if (d->out_mode == DBSR_OUT_NHWC) DBSR_CHECK_ARG(d->y.c0 + d->cout <= d->y.ld, "conv2d: output slice exceeds ld");
     if (d->out_mode == DBSR_OUT_NCHW_F32) DBSR_CHECK_ARG(d->y.dtype == DBSR_F32 && !d->res.ptr, "conv2d: NCHW out is f32, no residual");
     if (d->res.ptr) DBSR_CHECK_ARG(d->res.dtype == d->y.dtype && d->res.map.fpg > 0, "conv2d: residual dtype must equal output dtype");
+    if (d->gate.ptr)
+        DBSR_CHECK_ARG(d->gate.dtype == d->y.dtype && d->gate.map.fpg > 0 && d->out_mode == DBSR_OUT_NHWC && !d->precise,
+                       "conv2d: gate must be an NHWC tensor of the output dtype (NHWC output)");
     const long long npix = (long long)d->n_frames * d->out_h * d->out_w;
     DBSR_CHECK_ARG(npix < (1LL << 31), "conv2d: too many pixels");
 

@@ -1,0 +1,673 @@
+// Backward-pass and optimizer kernels for the DBSR training step (BASELINE configs[3]; SURVEY §8e/§8f
+// rank 3).  The reference trains with autograd over cuDNN/ATen (trainers/simple_trainer.py:78-81,
+// actors/dbsr_actors.py:27-47): L1 loss on the boundary-cropped prediction, loss.backward(), Adam.
+// Here every backward op is a hand-written HIP kernel; conv dgrad reuses the forward implicit-GEMM conv
+// (dbsr_conv2d with dgrad-packed weights and the gate epilogue), conv wgrad is the MFMA kernel below.
+// All activations NHWC (dbsr_hip.h); gradients of trainable parameters are fp32 in torch layout.
+#include "common.hpp"
+
+#include <algorithm>
+
+using namespace dbsr;
+
+namespace {
+
+inline unsigned nblocks(long long total, int bs) { return (unsigned)((total + bs - 1) / bs); }
+bool map_ok(const dbsr_tensor& t) { return t.ptr && t.map.fpg > 0; }
+bool vec_ok(const dbsr_tensor& t, int v) { return t.ld % v == 0 && t.c0 % v == 0; }
+
+template <typename F>
+int by_dtype(int dtype, F&& f) {
+    if (dtype == DBSR_BF16) return f((bf16_t*)nullptr);
+    if (dtype == DBSR_F32) return f((float*)nullptr);
+    dbsr_set_error("unsupported dtype %d", dtype);
+    return DBSR_E_ARG;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Conv weight gradient (nn.Conv2d backward w.r.t. weight, k = 1 or 3, stride 1, pad k/2):
+//   dW[co][ci][ky][kx] = sum over pixels p of dY[p][co] * X[p + (ky-1, kx-1)][ci]
+// a GEMM whose reduction axis is the pixel.  Work unit: a tile of 8 rows x 16 columns of one frame
+// (128 output pixels = 4 MFMA k-steps of 32).  A block owns a 64-cout x 64-cin slice and a contiguous
+// range of tiles; per tile it stages dY [128 px][64 co] and the (10 x 18)-pixel X halo [180 px][64 ci]
+// in LDS (rows of 64 channels, 16-B loads, zeros outside the frame / channel range), then
+//   3x3: wave t (9 waves) accumulates tap t: B rows are the halo pixels shifted by the tap;
+//   1x1: wave w (4 waves) accumulates k-step w of every tile.
+// bf16 MFMA 16x16x32 takes 8 consecutive pixels per lane for one channel: both operands are read from
+// the pixel-major tiles with the gfx950 transposed LDS read ds_read_b64_tr_b16 (two 4-row reads per
+// operand; cdna_hip_programming.md T10).  fp32 runs v_mfma_f32_16x16x4_f32 on plain reads (one pixel
+// per lane per MFMA).  Each wave's 64x64 accumulator block is written to its own fp32 partial slot
+// [block][wave][co][ci]; wgrad_reduce sums the slots in a fixed order (deterministic).
+// ------------------------------------------------------------------------------------------------
+constexpr int WG_TH = 8, WG_TW = 16, WG_PX = WG_TH * WG_TW;             // output tile
+constexpr int WG_HH = WG_TH + 2, WG_HW = WG_TW + 2, WG_HPX = WG_HH * WG_HW;   // halo
+
+template <typename T> struct WgCfg;
+template <> struct WgCfg<bf16_t> { static constexpr int ROWB = 144; };      // 128 B + 16 B skew per pixel row
+template <> struct WgCfg<float> { static constexpr int ROWB = 272; };       // 256 B + 16 B
+
+typedef short v4s_t __attribute__((ext_vector_type(4)));
+struct FragB { bf16x8_t v; };
+__device__ __forceinline__ f32x4_t mma_bf16(const FragB& a, const FragB& b, f32x4_t c) {
+    typedef __attribute__((ext_vector_type(8))) __bf16 bfv;
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bfv, a.v), __builtin_bit_cast(bfv, b.v), c, 0, 0, 0);
+}
+
+__device__ __forceinline__ v4s_t tr16(const unsigned char* lds_byte) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s_t*)lds_byte);
+}
+
+template <typename T, int K>
+__global__ __launch_bounds__(K == 3 ? 576 : 256) void conv_wgrad_kernel(
+        int n_frames, int h, int w, dbsr_tensor x, int cin, dbsr_tensor dy, int cout, long long n_units,
+        float* __restrict__ partial) {
+    constexpr int NW = K == 3 ? 9 : 4;
+    constexpr int ROWB = WgCfg<T>::ROWB;
+    __shared__ __attribute__((aligned(16))) unsigned char lds[(WG_PX + WG_HPX) * ROWB];
+    unsigned char* ldy = lds;                          // [128 px][64 co]
+    unsigned char* lx = lds + WG_PX * ROWB;            // [180 halo px][64 ci]
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int co0 = blockIdx.y * 64, ci0 = blockIdx.z * 64;
+    const int tiles_x = (w + WG_TW - 1) / WG_TW, tiles_y = (h + WG_TH - 1) / WG_TH;
+    const long long u0 = n_units * blockIdx.x / gridDim.x, u1 = n_units * (blockIdx.x + 1) / gridDim.x;
+    const int ky = K == 3 ? wave / 3 : 1, kx = K == 3 ? wave % 3 : 1;   // 1x1: centre "tap"
+    f32x4_t acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    constexpr int EPP = 16 / (int)sizeof(T);           // elements per 16-B piece
+    constexpr int PPR = 64 / EPP;                      // pieces per 64-channel row
+    for (long long u = u0; u < u1; ++u) {
+        const int tx = (int)(u % tiles_x);
+        long long r = u / tiles_x;
+        const int ty = (int)(r % tiles_y);
+        const int f = (int)(r / tiles_y);
+        const int y0 = ty * WG_TH, x0 = tx * WG_TW;
+        // ---- stage dY tile and X halo (zeros outside the frame and past cout / cin) ----
+        const T* dyf = img_ptr<T>(dy, f);
+        const T* xf = img_ptr<T>(x, f);
+        for (int it = threadIdx.x; it < (WG_PX + WG_HPX) * PPR; it += NW * 64) {
+            const int row = it / PPR, pc = it % PPR;
+            u32x4_t v = {0u, 0u, 0u, 0u};
+            if (row < WG_PX) {
+                const int yy = y0 + row / WG_TW, xx = x0 + row % WG_TW, c = co0 + pc * EPP;
+                if (yy < h && xx < w && c < cout) v = *(const u32x4_t*)(dyf + ((long long)yy * w + xx) * dy.ld + c);
+                *(u32x4_t*)(ldy + row * ROWB + pc * 16) = v;
+            } else {
+                const int hr = row - WG_PX;
+                const int yy = y0 - 1 + hr / WG_HW, xx = x0 - 1 + hr % WG_HW, c = ci0 + pc * EPP;
+                if ((unsigned)yy < (unsigned)h && (unsigned)xx < (unsigned)w && c < cin)
+                    v = *(const u32x4_t*)(xf + ((long long)yy * w + xx) * x.ld + c);
+                *(u32x4_t*)(lx + hr * ROWB + pc * 16) = v;
+            }
+        }
+        __syncthreads();
+        // ---- MFMAs ----
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            if (K == 1 && s != wave) continue;
+            if constexpr (sizeof(T) == 2) {
+                // lane (g = lane>>4, q = (lane>>2)&3, p = lane&3): rows k = 8g+q (+4) of this k-step,
+                // channels 4p..4p+3 of each 16-channel block
+                const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+                FragB a[4], b[4];
+#pragma unroll
+                for (int half = 0; half < 2; ++half) {
+                    const int kk = 8 * g + 4 * half + q;             // pixel of the k-step, 0..31
+                    const int ty_ = 2 * s + kk / 16, tx_ = kk % 16;
+                    const unsigned char* arow = ldy + (ty_ * WG_TW + tx_) * ROWB;
+                    const unsigned char* brow = lx + ((ty_ + ky) * WG_HW + tx_ + kx) * ROWB;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const v4s_t va = tr16(arow + (i * 16 + 4 * p) * 2);
+                        const v4s_t vb = tr16(brow + (i * 16 + 4 * p) * 2);
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            a[i].v[4 * half + e] = va[e];
+                            b[i].v[4 * half + e] = vb[e];
+                        }
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) acc[i][j] = mma_bf16(a[i], b[j], acc[i][j]);
+            } else {
+                // fp32: 8 MFMAs of k = 4 pixels; lane (kq = lane>>4, m = lane&15)
+                const int kq = lane >> 4, m = lane & 15;
+#pragma unroll
+                for (int k4 = 0; k4 < 8; ++k4) {
+                    const int kk = k4 * 4 + kq;
+                    const int ty_ = 2 * s + kk / 16, tx_ = kk % 16;
+                    const float* arow = (const float*)(ldy + (ty_ * WG_TW + tx_) * ROWB);
+                    const float* brow = (const float*)(lx + ((ty_ + ky) * WG_HW + tx_ + kx) * ROWB);
+                    float av[4], bv[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        av[i] = arow[i * 16 + m];
+                        bv[i] = brow[i * 16 + m];
+                    }
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+                }
+            }
+        }
+        __syncthreads();
+    }
+    // ---- this wave's partial: C[m = co][n = ci], lane holds co 4(lane>>4)+r of block i, ci lane&15 of block j
+    float* out = partial + ((long long)blockIdx.x * gridDim.y * gridDim.z + blockIdx.y * gridDim.z + blockIdx.z) *
+                               (NW * 64 * 64) + wave * 64 * 64;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                out[(i * 16 + 4 * (lane >> 4) + r) * 64 + j * 16 + (lane & 15)] = acc[i][j][r];
+}
+
+// dW[co][ci][tap] (+)= sum over blocks (and, for 1x1, over the 4 waves) of the partial slots
+__global__ void wgrad_reduce_kernel(int nbx, int nty, int ntz, int nw, int taps, int cout, int cin,
+                                    const float* __restrict__ partial, float* __restrict__ dw, int accumulate) {
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long long)cout * cin * taps) return;
+    const int tap = (int)(idx % taps);
+    const int ci = (int)((idx / taps) % cin), co = (int)(idx / ((long long)taps * cin));
+    const int by = co / 64, bz = ci / 64, cl = co % 64, il = ci % 64;
+    float s = 0.f;
+    for (int bx = 0; bx < nbx; ++bx) {
+        const float* blk = partial + ((long long)bx * nty * ntz + by * ntz + bz) * (nw * 64 * 64);
+        if (taps == 1) {
+            for (int wv = 0; wv < nw; ++wv) s += blk[wv * 4096 + cl * 64 + il];
+        } else {
+            s += blk[tap * 4096 + cl * 64 + il];
+        }
+    }
+    dw[idx] = accumulate ? dw[idx] + s : s;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Per-channel sum over all pixels (conv bias gradient, db[c] = sum_p dY[p][c]): block = (64 channels,
+// pixel range), partials [nblk][c], reduced in block order.
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void chan_sum_kernel(int n, int hw, int c, dbsr_tensor t, int px_per_block,
+                                                       float* __restrict__ partial) {
+    const int cl = threadIdx.x & 63, sub = threadIdx.x >> 6;
+    const int ch = blockIdx.y * 64 + cl;
+    const long long total = (long long)n * hw;
+    const long long p0 = (long long)blockIdx.x * px_per_block, p1 = std::min<long long>(p0 + px_per_block, total);
+    float s = 0.f;
+    if (ch < c)
+        for (long long p = p0 + sub; p < p1; p += 4) {
+            const int f = (int)(p / hw), rr = (int)(p - (long long)f * hw);
+            s += elem<T>::ld(img_ptr<T>(t, f) + (long long)rr * t.ld + ch);
+        }
+    __shared__ float red[4][64];
+    red[sub][cl] = s;
+    __syncthreads();
+    if (sub == 0 && ch < c) partial[(long long)blockIdx.x * c + ch] = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+}
+
+__global__ void sum_rows_kernel(int rows, int c, const float* __restrict__ partial, float* __restrict__ out,
+                                int accumulate, float scale) {
+    const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+    if (ch >= c) return;
+    float s = 0.f;
+    for (int r = 0; r < rows; ++r) s += partial[(long long)r * c + ch];
+    s *= scale;
+    out[ch] = accumulate ? out[ch] + s : s;
+}
+
+// ------------------------------------------------------------------------------------------------
+// L1 loss on the boundary-cropped prediction (models/loss/image_quality_v2.py:24-66, boundary_ignore
+// 40, mean reduction) and its gradient through the predictor's ReLU (decoders.py:52, blocks.py:46):
+//   d_pre[b,c,y,x] = [pred > 0] * sign(pred - gt) / count inside the crop, 0 outside
+// written NHWC (ld >= 4, compute dtype) for the predictor's dgrad / wgrad; |pred - gt| partial sums
+// per block into `partial` (the loss is their ordered sum / count).
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void l1_loss_bwd_kernel(int B, int C, int H, int W, int bi,
+                                                          const float* __restrict__ pred, const float* __restrict__ gt,
+                                                          float inv_count, dbsr_tensor dpre,
+                                                          float* __restrict__ partial) {
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long total = (long long)B * H * W;
+    float s = 0.f;
+    if (idx < total) {
+        const int b = (int)(idx / ((long long)H * W));
+        const int rr = (int)(idx - (long long)b * H * W);
+        const int y = rr / W, x = rr - y * W;
+        const bool in = y >= bi && y < H - bi && x >= bi && x < W - bi;
+        T* o = img_ptr<T>(dpre, b) + (long long)rr * dpre.ld;
+        for (int c = 0; c < C; ++c) {
+            const long long off = ((long long)b * C + c) * H * W + rr;
+            const float d = pred[off] - gt[off];
+            float gv = 0.f;
+            if (in) {
+                s += fabsf(d);
+                gv = pred[off] > 0.f ? (d > 0.f ? inv_count : (d < 0.f ? -inv_count : 0.f)) : 0.f;
+            }
+            elem<T>::st(o + c, gv);
+        }
+    }
+    __shared__ float red[256];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int st = 128; st > 0; st >>= 1) {
+        if ((int)threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+
+// ------------------------------------------------------------------------------------------------
+// PixelShuffle(s) backward with the upsampler's ReLU (upsampling.py:51-58): the gradient of the
+// shuffled, ReLU'd output dS [B][sH][sW][C] (and the forward output S itself as the gate) -> the conv's
+// pre-activation gradient in torch channel order k = c*s^2 + i*s + j: dU[b][y][x][k] =
+// dS[b][y*s+i][x*s+j][c] * [S > 0].
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void unshuffle_gate_kernel(int B, int H, int W, int s, int C, dbsr_tensor ds,
+                                                             dbsr_tensor gate, dbsr_tensor du) {
+    const int K = C * s * s;
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long long)B * H * W * K) return;
+    const int k = (int)(idx % K);
+    const long long pix = idx / K;
+    const int b = (int)(pix / ((long long)H * W)), rr = (int)(pix - (long long)b * H * W);
+    const int y = rr / W, x = rr - y * W;
+    const int c = k / (s * s), sub = k - c * s * s, i = sub / s, j = sub - i * s;
+    const long long hr = (long long)(y * s + i) * (W * s) + (x * s + j);
+    const float g = elem<T>::ld(img_ptr<T>(gate, b) + hr * gate.ld + c);
+    const float v = g > 0.f ? elem<T>::ld(img_ptr<T>(ds, b) + hr * ds.ld + c) : 0.f;
+    elem<T>::st(img_ptr<T>(du, b) + (long long)rr * du.ld + k, v);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Softmax-fusion backward (merging.py:116-124): fused = sum_n w_n f_n, w = softmax_n(l) per channel.
+//   dF_n = w_n * dfused;  dl_n = w_n * dfused * (f_n - fused)
+// Frame (b, n): weights/logit-grad image b*N+n; feature n == 0 -> ref image b (map), n > 0 -> oth image
+// b*(N-1)+n-1; dref: image b; doth: image b*(N-1)+n-1.  8 channels per thread.
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void fuse_bwd_kernel(int B, int N, int hw, int C, dbsr_tensor wts, dbsr_tensor ref,
+                                                       dbsr_tensor oth, dbsr_tensor fused, dbsr_tensor dfused,
+                                                       dbsr_tensor dlogits, dbsr_tensor dref, dbsr_tensor doth) {
+    const int groups = C / 8;
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long long)B * hw * groups) return;
+    const int g = (int)(idx % groups);
+    const long long pix = idx / groups;
+    const int b = (int)(pix / hw), rr = (int)(pix - (long long)b * hw);
+    const int c = g * 8;
+    float fu[8], dfu[8];
+    load8(img_ptr<T>(fused, b) + (long long)rr * fused.ld + c, fu);
+    load8(img_ptr<T>(dfused, b) + (long long)rr * dfused.ld + c, dfu);
+    for (int n = 0; n < N; ++n) {
+        float wv[8], fv[8], dl[8], df[8];
+        load8(img_ptr<T>(wts, b * N + n) + (long long)rr * wts.ld + c, wv);
+        const T* fp = n == 0 ? img_ptr<T>(ref, b) + (long long)rr * ref.ld
+                             : img_ptr<T>(oth, b * (N - 1) + n - 1) + (long long)rr * oth.ld;
+        load8(fp + c, fv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            df[j] = wv[j] * dfu[j];
+            dl[j] = df[j] * (fv[j] - fu[j]);
+        }
+        store8(img_ptr<T>(dlogits, b * N + n) + (long long)rr * dlogits.ld + c, dl);
+        T* dp = n == 0 ? img_ptr<T>(dref, b) + (long long)rr * dref.ld
+                       : img_ptr<T>(doth, b * (N - 1) + n - 1) + (long long)rr * doth.ld;
+        store8(dp + c, df);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// merge-prep backward (merging.py:79-89) + the projection's ReLU: weight-predictor input gradient
+// dwp [b*N+n][base(c) | diff(c) | ...] ->
+//   d_proj[b,0] = sum_n d_base[b,n] - sum_{n>=1} d_diff[b,n];  d_proj[b,n>=1] = d_diff[b,n]
+// times [proj > 0], into dproj (images b*N+n).
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void merge_prep_bwd_kernel(int B, int N, int hw, int C, dbsr_tensor dwp,
+                                                             dbsr_tensor proj, dbsr_tensor dproj) {
+    const int groups = C / 8;
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long long)B * N * hw * groups) return;
+    const int g = (int)(idx % groups);
+    const long long pix = idx / groups;
+    const int f = (int)(pix / hw), rr = (int)(pix - (long long)f * hw);
+    const int b = f / N, n = f - b * N;
+    const int c = g * 8;
+    float d[8];
+    if (n > 0) {
+        load8(img_ptr<T>(dwp, f) + (long long)rr * dwp.ld + C + c, d);
+    } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d[j] = 0.f;
+        for (int m = 0; m < N; ++m) {
+            float db[8], dd[8];
+            load8(img_ptr<T>(dwp, b * N + m) + (long long)rr * dwp.ld + c, db);
+            load8(img_ptr<T>(dwp, b * N + m) + (long long)rr * dwp.ld + C + c, dd);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) d[j] += db[j] - (m > 0 ? dd[j] : 0.f);
+        }
+    }
+    float pv[8];
+    load8(img_ptr<T>(proj, f) + (long long)rr * proj.ld + c, pv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d[j] = pv[j] > 0.f ? d[j] : 0.f;
+    store8(img_ptr<T>(dproj, f) + (long long)rr * dproj.ld + c, d);
+}
+
+// ------------------------------------------------------------------------------------------------
+// warp backward w.r.t. the features (models/layers/warp.py:19-46 = grid_sample bilinear, zeros,
+// align_corners=False at (x + fx, y + fy)): dfeat[src] += w_tap * dout[p] for the 4 taps of every
+// output pixel -- fp32 atomics into dfeat32 (the scatter has no gather form for arbitrary flow), 8
+// channels per thread.
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void warp_bwd_kernel(int n, int h, int w, int C, dbsr_tensor dout,
+                                                       const float* __restrict__ flow, long long fis,
+                                                       float* __restrict__ dfeat32, dbsr_frame_map fmap,
+                                                       long long df_img_stride) {
+    const int groups = C / 8;
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long long)n * h * w * groups) return;
+    const int g = (int)(idx % groups);
+    const long long pix = idx / groups;
+    const int hw = h * w;
+    const int p = (int)(pix / hw), rr = (int)(pix - (long long)p * hw);
+    const int y = rr / w, x = rr - y * w;
+    const float* fl = flow + (long long)p * fis + rr;
+    const float gx = ((float)x + 0.5f) + fl[0], gy = ((float)y + 0.5f) + fl[hw];
+    const float gxn = 2.0f * gx / (float)w - 1.0f, gyn = 2.0f * gy / (float)h - 1.0f;
+    const float ix = ((gxn + 1.f) * (float)w - 1.f) / 2.f, iy = ((gyn + 1.f) * (float)h - 1.f) / 2.f;
+    const float fx0 = floorf(ix), fy0 = floorf(iy);
+    const int x0 = (int)fx0, y0 = (int)fy0;
+    const float wx1 = ix - fx0, wx0 = 1.f - wx1, wy1 = iy - fy0, wy0 = 1.f - wy1;
+    float d[8];
+    load8(img_ptr<T>(dout, p) + (long long)rr * dout.ld + g * 8, d);
+    float* base = dfeat32 + map_frame(fmap, p) * df_img_stride + g * 8;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const int xx = x0 + (t & 1), yy = y0 + (t >> 1);
+        if ((unsigned)xx >= (unsigned)w || (unsigned)yy >= (unsigned)h) continue;
+        const float wt = ((t & 1) ? wx1 : wx0) * ((t >> 1) ? wy1 : wy0);
+        float* o = base + ((long long)yy * w + xx) * C;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) atomicAdd(o + j, wt * d[j]);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Encoder output gradient assembly (encoders.py:66-80 + the out_layer ReLU): frame (b, n):
+//   n == 0: dE = dref[b];  n >= 1: dE = dsrc32[b*N+n] (the warp scatter)
+// times [E > 0], into dE (images b*N+n).
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void enc_grad_gate_kernel(int B, int N, int hw, int C, dbsr_tensor dref,
+                                                            const float* __restrict__ dsrc32, dbsr_tensor e,
+                                                            dbsr_tensor de) {
+    const int groups = C / 8;
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long long)B * N * hw * groups) return;
+    const int g = (int)(idx % groups);
+    const long long pix = idx / groups;
+    const int f = (int)(pix / hw), rr = (int)(pix - (long long)f * hw);
+    const int b = f / N, n = f - b * N;
+    float d[8];
+    if (n == 0) {
+        load8(img_ptr<T>(dref, b) + (long long)rr * dref.ld + g * 8, d);
+    } else {
+        const float* s = dsrc32 + ((long long)f * hw + rr) * C + g * 8;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d[j] = s[j];
+    }
+    float ev[8];
+    load8(img_ptr<T>(e, f) + (long long)rr * e.ld + g * 8, ev);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d[j] = ev[j] > 0.f ? d[j] : 0.f;
+    store8(img_ptr<T>(de, f) + (long long)rr * de.ld + g * 8, d);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Adam (torch.optim.Adam, weight_decay 0, amsgrad False; trainers/simple_trainer.py:81 with the
+// default_synthetic.py:94 optimizer): on flat fp32 parameter / gradient / moment buffers.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void adam_kernel(long long n, float* __restrict__ p, const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v, float lr, float b1,
+                                                   float b2, float eps, float bc1, float bc2_sqrt, float gscale) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float gi = g[i] * gscale;
+    const float mi = b1 * m[i] + (1.f - b1) * gi;
+    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    // torch: p -= lr / bc1 * m / (sqrt(v) / sqrt(bc2) + eps)
+    p[i] -= (lr / bc1) * mi / (sqrtf(vi) / bc2_sqrt + eps);
+}
+
+// dgrad weights: the conv of the output gradient with the transposed, spatially flipped kernel
+// W'[ci][co][ky][kx] = W[co][ci][kh-1-ky][kw-1-kx] (fp32 torch layout in and out)
+__global__ void dgrad_weights_kernel(const float* __restrict__ w, int cout, int cin, int kh, int kw,
+                                     float* __restrict__ wt) {
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long long)cout * cin * kh * kw) return;
+    const int kx = (int)(idx % kw), ky = (int)((idx / kw) % kh);
+    const int co = (int)((idx / ((long long)kw * kh)) % cout), ci = (int)(idx / ((long long)kw * kh * cout));
+    wt[idx] = w[(((long long)co * cin + ci) * kh + (kh - 1 - ky)) * kw + (kw - 1 - kx)];
+}
+
+}  // namespace
+
+// ================================================================================================
+extern "C" size_t dbsr_conv_wgrad_workspace_bytes(int n_frames, int h, int w, int cin, int cout, int k) {
+    if (n_frames <= 0 || h <= 0 || w <= 0 || cin <= 0 || cout <= 0 || (k != 1 && k != 3)) return 0;
+    const long long units = (long long)n_frames * ((h + WG_TH - 1) / WG_TH) * ((w + WG_TW - 1) / WG_TW);
+    const int nty = (cout + 63) / 64, ntz = (cin + 63) / 64;
+    const long long nbx = std::max<long long>(1, std::min<long long>(units, std::max(1, 1024 / (nty * ntz))));
+    const int nw = k == 3 ? 9 : 4;
+    return (size_t)nbx * nty * ntz * nw * 64 * 64 * sizeof(float);
+}
+
+extern "C" int dbsr_conv_wgrad(int n_frames, int h, int w, dbsr_tensor x, int cin, dbsr_tensor dy, int cout, int k,
+                               float* dw, int accumulate, void* workspace, size_t workspace_bytes, void* stream) {
+    DBSR_CHECK_ARG(map_ok(x) && map_ok(dy) && dw && workspace, "conv_wgrad: null pointer");
+    DBSR_CHECK_ARG(x.dtype == dy.dtype, "conv_wgrad: x and dy dtypes differ");
+    DBSR_CHECK_ARG(k == 1 || k == 3, "conv_wgrad: k must be 1 or 3 (stride 1, pad k/2)");
+    DBSR_CHECK_ARG(n_frames > 0 && h > 0 && w > 0 && cin > 0 && cout > 0, "conv_wgrad: bad sizes");
+    const int esz = x.dtype == DBSR_BF16 ? 2 : 4, epp = 16 / esz;
+    DBSR_CHECK_ARG(vec_ok(x, epp) && vec_ok(dy, epp) && x.ld >= x.c0 + (cin + epp - 1) / epp * epp &&
+                   dy.ld >= dy.c0 + (cout + epp - 1) / epp * epp,
+                   "conv_wgrad: ld/c0 must be multiples of %d and cover the channels", epp);
+    const size_t need = dbsr_conv_wgrad_workspace_bytes(n_frames, h, w, cin, cout, k);
+    DBSR_CHECK_ARG(workspace_bytes >= need, "conv_wgrad: workspace %zu < %zu bytes", workspace_bytes, need);
+    const long long units = (long long)n_frames * ((h + WG_TH - 1) / WG_TH) * ((w + WG_TW - 1) / WG_TW);
+    const int nty = (cout + 63) / 64, ntz = (cin + 63) / 64;
+    const int nbx = (int)std::max<long long>(1, std::min<long long>(units, std::max(1, 1024 / (nty * ntz))));
+    const int nw = k == 3 ? 9 : 4;
+    float* part = (float*)workspace;
+    hipStream_t s = (hipStream_t)stream;
+    // the channel slice is folded into the base pointers
+    dbsr_tensor xx = x, dd = dy;
+    xx.ptr = (char*)x.ptr + (long long)x.c0 * esz;
+    xx.c0 = 0;
+    dd.ptr = (char*)dy.ptr + (long long)dy.c0 * esz;
+    dd.c0 = 0;
+    const dim3 grid(nbx, nty, ntz);
+    int rc = by_dtype(x.dtype, [&](auto* tag) {
+        using T = std::remove_pointer_t<decltype(tag)>;
+        if (k == 3)
+            hipLaunchKernelGGL((conv_wgrad_kernel<T, 3>), grid, dim3(576), 0, s, n_frames, h, w, xx, cin, dd, cout,
+                               units, part);
+        else
+            hipLaunchKernelGGL((conv_wgrad_kernel<T, 1>), grid, dim3(256), 0, s, n_frames, h, w, xx, cin, dd, cout,
+                               units, part);
+        DBSR_LAUNCH_CHECK();
+        return 0;
+    });
+    if (rc) return rc;
+    const long long total = (long long)cout * cin * k * k;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(nblocks(total, 256)), dim3(256), 0, s, nbx, nty, ntz, nw, k * k, cout,
+                       cin, part, dw, accumulate);
+    DBSR_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" size_t dbsr_chan_sum_workspace_bytes(int n, int hw, int c) {
+    const long long total = (long long)n * hw;
+    const long long nbx = std::min<long long>(512, std::max<long long>(1, (total + 255) / 256));
+    return (size_t)nbx * c * sizeof(float);
+}
+
+extern "C" int dbsr_chan_sum(int n, int hw, int c, dbsr_tensor t, float* out, int accumulate, void* workspace,
+                             size_t workspace_bytes, void* stream) {
+    DBSR_CHECK_ARG(map_ok(t) && out && workspace && n > 0 && hw > 0 && c > 0, "chan_sum: bad arguments");
+    DBSR_CHECK_ARG(workspace_bytes >= dbsr_chan_sum_workspace_bytes(n, hw, c), "chan_sum: workspace too small");
+    const long long total = (long long)n * hw;
+    const int nbx = (int)std::min<long long>(512, std::max<long long>(1, (total + 255) / 256));
+    const int ppb = (int)((total + nbx - 1) / nbx);
+    hipStream_t s = (hipStream_t)stream;
+    int rc = by_dtype(t.dtype, [&](auto* tag) {
+        using T = std::remove_pointer_t<decltype(tag)>;
+        hipLaunchKernelGGL((chan_sum_kernel<T>), dim3(nbx, (c + 63) / 64), dim3(256), 0, s, n, hw, c, t, ppb,
+                           (float*)workspace);
+        DBSR_LAUNCH_CHECK();
+        return 0;
+    });
+    if (rc) return rc;
+    hipLaunchKernelGGL(sum_rows_kernel, dim3(nblocks(c, 256)), dim3(256), 0, s, nbx, c, (const float*)workspace, out,
+                       accumulate, 1.0f);
+    DBSR_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int dbsr_l1_loss_backward(int B, int C, int H, int W, int boundary_ignore, const float* pred,
+                                     const float* gt, dbsr_tensor dpre, float* loss, void* workspace,
+                                     size_t workspace_bytes, void* stream) {
+    DBSR_CHECK_ARG(pred && gt && loss && workspace && map_ok(dpre), "l1_loss_backward: null pointer");
+    DBSR_CHECK_ARG(B > 0 && C > 0 && H > 2 * boundary_ignore && W > 2 * boundary_ignore && boundary_ignore >= 0 &&
+                   dpre.ld >= dpre.c0 + C, "l1_loss_backward: bad sizes");
+    const long long total = (long long)B * H * W;
+    const unsigned nb = nblocks(total, 256);
+    DBSR_CHECK_ARG(workspace_bytes >= nb * sizeof(float), "l1_loss_backward: workspace < %u floats", nb);
+    const float count = (float)B * C * (H - 2 * boundary_ignore) * (W - 2 * boundary_ignore);
+    hipStream_t s = (hipStream_t)stream;
+    int rc = by_dtype(dpre.dtype, [&](auto* tag) {
+        using T = std::remove_pointer_t<decltype(tag)>;
+        hipLaunchKernelGGL((l1_loss_bwd_kernel<T>), dim3(nb), dim3(256), 0, s, B, C, H, W, boundary_ignore, pred, gt,
+                           1.0f / count, dpre, (float*)workspace);
+        DBSR_LAUNCH_CHECK();
+        return 0;
+    });
+    if (rc) return rc;
+    hipLaunchKernelGGL(sum_rows_kernel, dim3(1), dim3(256), 0, s, (int)nb, 1, (const float*)workspace, loss, 0,
+                       1.0f / count);
+    DBSR_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int dbsr_unshuffle_gate(int B, int H, int W, int s, int c, dbsr_tensor ds, dbsr_tensor gate, dbsr_tensor du,
+                                   void* stream) {
+    DBSR_CHECK_ARG(map_ok(ds) && map_ok(gate) && map_ok(du) && ds.dtype == gate.dtype && ds.dtype == du.dtype,
+                   "unshuffle_gate: bad tensors");
+    DBSR_CHECK_ARG(B > 0 && H > 0 && W > 0 && s > 0 && c > 0 && du.ld >= du.c0 + c * s * s, "unshuffle_gate: sizes");
+    const long long total = (long long)B * H * W * c * s * s;
+    return by_dtype(ds.dtype, [&](auto* tag) {
+        using T = std::remove_pointer_t<decltype(tag)>;
+        hipLaunchKernelGGL((unshuffle_gate_kernel<T>), dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, B,
+                           H, W, s, c, ds, gate, du);
+        DBSR_LAUNCH_CHECK();
+        return 0;
+    });
+}
+
+extern "C" int dbsr_fuse_backward(int B, int N, int hw, int c, dbsr_tensor weights, dbsr_tensor ref, dbsr_tensor oth,
+                                  dbsr_tensor fused, dbsr_tensor dfused, dbsr_tensor dlogits, dbsr_tensor dref,
+                                  dbsr_tensor doth, void* stream) {
+    DBSR_CHECK_ARG(map_ok(weights) && map_ok(ref) && map_ok(fused) && map_ok(dfused) && map_ok(dlogits) &&
+                   map_ok(dref) && (N == 1 || (map_ok(oth) && map_ok(doth))), "fuse_backward: bad tensors");
+    DBSR_CHECK_ARG(B > 0 && N > 0 && hw > 0 && c % 8 == 0, "fuse_backward: c must be a multiple of 8");
+    const dbsr_tensor* ts[] = {&weights, &ref, &fused, &dfused, &dlogits, &dref};
+    for (auto* t : ts) DBSR_CHECK_ARG(t->dtype == ref.dtype && vec_ok(*t, 8), "fuse_backward: dtype/layout");
+    const long long total = (long long)B * hw * (c / 8);
+    return by_dtype(ref.dtype, [&](auto* tag) {
+        using T = std::remove_pointer_t<decltype(tag)>;
+        hipLaunchKernelGGL((fuse_bwd_kernel<T>), dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, B, N, hw,
+                           c, weights, ref, oth, fused, dfused, dlogits, dref, doth);
+        DBSR_LAUNCH_CHECK();
+        return 0;
+    });
+}
+
+extern "C" int dbsr_merge_prep_backward(int B, int N, int hw, int c, dbsr_tensor dwp, dbsr_tensor proj,
+                                        dbsr_tensor dproj, void* stream) {
+    DBSR_CHECK_ARG(map_ok(dwp) && map_ok(proj) && map_ok(dproj) && dwp.dtype == proj.dtype && dproj.dtype == proj.dtype,
+                   "merge_prep_backward: bad tensors");
+    DBSR_CHECK_ARG(c % 8 == 0 && vec_ok(dwp, 8) && vec_ok(proj, 8) && vec_ok(dproj, 8) && dwp.ld >= dwp.c0 + 2 * c,
+                   "merge_prep_backward: layout");
+    const long long total = (long long)B * N * hw * (c / 8);
+    return by_dtype(proj.dtype, [&](auto* tag) {
+        using T = std::remove_pointer_t<decltype(tag)>;
+        hipLaunchKernelGGL((merge_prep_bwd_kernel<T>), dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, B,
+                           N, hw, c, dwp, proj, dproj);
+        DBSR_LAUNCH_CHECK();
+        return 0;
+    });
+}
+
+extern "C" int dbsr_warp_backward(int n, int h, int w, int c, dbsr_tensor dout, const float* flow,
+                                  long long flow_img_stride, float* dfeat32, dbsr_frame_map fmap,
+                                  long long dfeat_img_stride, void* stream) {
+    DBSR_CHECK_ARG(map_ok(dout) && flow && dfeat32 && fmap.fpg > 0, "warp_backward: bad tensors");
+    DBSR_CHECK_ARG(n > 0 && h > 0 && w > 0 && c % 8 == 0 && vec_ok(dout, 8), "warp_backward: layout");
+    const long long total = (long long)n * h * w * (c / 8);
+    return by_dtype(dout.dtype, [&](auto* tag) {
+        using T = std::remove_pointer_t<decltype(tag)>;
+        hipLaunchKernelGGL((warp_bwd_kernel<T>), dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, n, h, w,
+                           c, dout, flow, flow_img_stride, dfeat32, fmap, dfeat_img_stride);
+        DBSR_LAUNCH_CHECK();
+        return 0;
+    });
+}
+
+extern "C" int dbsr_enc_grad_gate(int B, int N, int hw, int c, dbsr_tensor dref, const float* dsrc32, dbsr_tensor e,
+                                  dbsr_tensor de, void* stream) {
+    DBSR_CHECK_ARG(map_ok(dref) && dsrc32 && map_ok(e) && map_ok(de) && dref.dtype == e.dtype && de.dtype == e.dtype,
+                   "enc_grad_gate: bad tensors");
+    DBSR_CHECK_ARG(c % 8 == 0 && vec_ok(dref, 8) && vec_ok(e, 8) && vec_ok(de, 8), "enc_grad_gate: layout");
+    const long long total = (long long)B * N * hw * (c / 8);
+    return by_dtype(e.dtype, [&](auto* tag) {
+        using T = std::remove_pointer_t<decltype(tag)>;
+        hipLaunchKernelGGL((enc_grad_gate_kernel<T>), dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, B,
+                           N, hw, c, dref, dsrc32, e, de);
+        DBSR_LAUNCH_CHECK();
+        return 0;
+    });
+}
+
+extern "C" int dbsr_adam_step(long long n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                              float lr, float beta1, float beta2, float eps, int step, float grad_scale,
+                              void* stream) {
+    DBSR_CHECK_ARG(n > 0 && param && grad && exp_avg && exp_avg_sq && step >= 1, "adam_step: bad arguments");
+    const float bc1 = 1.f - powf(beta1, (float)step), bc2 = 1.f - powf(beta2, (float)step);
+    hipLaunchKernelGGL(adam_kernel, dim3(nblocks(n, 256)), dim3(256), 0, (hipStream_t)stream, n, param, grad, exp_avg,
+                       exp_avg_sq, lr, beta1, beta2, eps, bc1, sqrtf(bc2), grad_scale);
+    DBSR_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int dbsr_dgrad_weights(const float* w, int cout, int cin, int kh, int kw, float* wt, void* stream) {
+    DBSR_CHECK_ARG(w && wt && cout > 0 && cin > 0 && kh > 0 && kw > 0, "dgrad_weights: bad arguments");
+    const long long total = (long long)cout * cin * kh * kw;
+    hipLaunchKernelGGL(dgrad_weights_kernel, dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, w, cout, cin,
+                       kh, kw, wt);
+    DBSR_LAUNCH_CHECK();
+    return 0;
+}

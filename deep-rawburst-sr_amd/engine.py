@@ -157,10 +157,11 @@ class Plan:
 
     def conv(self, name, pc, n_frames, x, xc0, in_hw, y, yc0, act, xmap=IDENTITY, ymap=IDENTITY, res=None,
              rc0=0, rmap=IDENTITY, post_act=L.ACT_NONE, out_mode=L.OUT_NHWC, shuffle=0, y_desc=None, cin=None,
-             precise=False, head=None):
+             precise=False, head=None, gate=None, gc0=0, gmap=IDENTITY):
         """Emit one conv.  head = (name, w [hc, cout] fp32, b [hc] | None, out_desc): when the library can fuse
         it (dbsr_conv_head_ok), the conv's own output is not stored and the 1x1 head + ReLU writes out_desc
-        (fp32 NCHW); the returned desc then has .fused_head = True."""
+        (fp32 NCHW); the returned desc then has .fused_head = True.  gate: output *= (gate > 0) (training
+        dgrad: the ReLU backward of the layer that produced the forward conv's input)."""
         oh, ow = pc.out_hw(*in_hw)
         assert cin is None or cin == pc.cin, (name, cin, pc.cin)
         d = L.ConvDesc()
@@ -175,6 +176,7 @@ class Plan:
         d.out_h, d.out_w = oh, ow               # (OUT_SHUFFLE: the kernel scales by `shuffle` itself)
         d.act = act
         d.res = res.d(rc0, rmap) if res is not None else L.NULL_TENSOR
+        d.gate = gate.d(gc0, gmap) if gate is not None else L.NULL_TENSOR
         d.post_act = post_act
         d.out_mode, d.shuffle = out_mode, shuffle
         d.workspace, d.workspace_bytes = None, 0

@@ -136,3 +136,107 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, act=L.ACT_NONE
         return out
     L.check(L.lib().dbsr_conv2d(d, s), 'dbsr_conv2d')
     return y[..., :pc].permute(0, 3, 1, 2).contiguous()
+
+
+# ---------------------------------------------------------------------------------------------------
+# training-step kernels (backward of the ops above; dbsr_hip.h 'training step')
+# ---------------------------------------------------------------------------------------------------
+def conv2d_wgrad(x, dy, k, compute_dtype=torch.float32):
+    """dL/dW of nn.Conv2d(k x k, stride 1, pad k//2) for input x [N,Cin,H,W] and output gradient dy
+    [N,Cout,H,W] (dbsr_conv_wgrad): fp32 [Cout,Cin,k,k]."""
+    _need_cuda(x, dy)
+    N, Cin, H, W = x.shape
+    Cout = dy.shape[1]
+    xs, ldx = _nhwc(x, compute_dtype)
+    ds, ldd = _nhwc(dy, compute_dtype)
+    dw = torch.zeros(Cout, Cin, k, k, dtype=torch.float32, device=x.device)
+    need = L.lib().dbsr_conv_wgrad_workspace_bytes(N, H, W, Cin, Cout, k)
+    ws = torch.empty(max(need // 4, 1), dtype=torch.float32, device=x.device)
+    L.check(L.lib().dbsr_conv_wgrad(N, H, W, L.tensor_desc(xs, ldx), Cin, L.tensor_desc(ds, ldd), Cout, k,
+                                    dw.data_ptr(), 0, ws.data_ptr(), need, L.stream_ptr(x.device)), 'dbsr_conv_wgrad')
+    return dw
+
+
+def conv2d_dgrad(dy, weight, residual=None, gate=None, compute_dtype=torch.float32):
+    """dL/dX of nn.Conv2d(weight, stride 1, pad k//2) for output gradient dy [N,Cout,H,W]: the forward conv
+    kernel on dgrad-packed weights (dbsr_dgrad_weights + dbsr_conv_pack_weights), then + residual and
+    * (gate > 0) in its epilogue (the ResBlock / ReLU backward).  NCHW fp32/bf16 out."""
+    _need_cuda(dy, weight)
+    Cout, Cin, kh, kw = weight.shape
+    w32 = weight.to(torch.float32).contiguous()
+    wt = torch.empty(Cin, Cout, kh, kw, dtype=torch.float32, device=dy.device)
+    s = L.stream_ptr(dy.device)
+    L.check(L.lib().dbsr_dgrad_weights(w32.data_ptr(), Cout, Cin, kh, kw, wt.data_ptr(), s), 'dbsr_dgrad_weights')
+    N, _, H, W = dy.shape
+    ds, ldd = _nhwc(dy, compute_dtype)
+    n = L.lib().dbsr_conv_packed_elems(Cin, Cout, kh, kw)
+    wp = torch.empty(n, dtype=compute_dtype, device=dy.device)
+    L.check(L.lib().dbsr_conv_pack_weights(wt.data_ptr(), None, Cin, Cout, kh, kw, L.dtype_code(compute_dtype), 1,
+                                           wp.data_ptr(), None, s), 'pack')
+    ldy = (Cin + 7) // 8 * 8
+    y = torch.zeros(N, H, W, ldy, dtype=compute_dtype, device=dy.device)
+    d = L.ConvDesc()
+    d.n_frames = N
+    d.x = L.tensor_desc(ds, ldd)
+    d.in_h, d.in_w, d.cin = H, W, Cout
+    d.w, d.bias = wp.data_ptr(), None
+    d.cout, d.kh, d.kw, d.stride, d.pad, d.dil = Cin, kh, kw, 1, kh // 2, 1
+    d.y = L.tensor_desc(y, ldy)
+    d.out_h, d.out_w = H, W
+    d.act, d.post_act = L.ACT_NONE, L.ACT_NONE
+    keep = []
+    if residual is not None:
+        rr, ldr = _nhwc(residual, compute_dtype)
+        if ldr != ldy:
+            rr = torch.nn.functional.pad(rr, (0, ldy - ldr)) if ldr < ldy else rr[..., :ldy].contiguous()
+        d.res = L.tensor_desc(rr, ldy)
+        keep.append(rr)
+    if gate is not None:
+        gg, ldg = _nhwc(gate, compute_dtype)
+        if ldg != ldy:
+            gg = torch.nn.functional.pad(gg, (0, ldy - ldg)) if ldg < ldy else gg[..., :ldy].contiguous()
+        d.gate = L.tensor_desc(gg, ldy)
+        keep.append(gg)
+    d.out_mode, d.shuffle = L.OUT_NHWC, 0
+    need = L.lib().dbsr_conv_workspace_bytes(d)
+    ws = torch.zeros(max(need // 4, 1), dtype=torch.float32, device=dy.device)
+    d.workspace, d.workspace_bytes = ws.data_ptr(), need
+    L.check(L.lib().dbsr_conv2d(d, s), 'dbsr_conv2d (dgrad)')
+    return y[..., :Cin].permute(0, 3, 1, 2).contiguous()
+
+
+def fuse_backward(weights, all_feat, fused, dfused):
+    """Softmax-fusion backward (merging.py:116-124): weights / all_feat [B,N,C,H,W], fused / dfused [B,C,H,W]
+    -> (dlogits [B,N,C,H,W], dfeat [B,N,C,H,W])."""
+    _need_cuda(weights, all_feat, fused, dfused)
+    B, N, C, H, W = all_feat.shape
+    dt = all_feat.dtype
+    nh = lambda t: t.reshape(-1, C, H, W).permute(0, 2, 3, 1).contiguous()          # noqa: E731
+    w, f = nh(weights.to(dt)), nh(all_feat)
+    fu, dfu = nh(fused.to(dt)), nh(dfused.to(dt))
+    dl = torch.empty_like(w)
+    df = torch.empty_like(f)
+    img = H * W * C
+    L.check(L.lib().dbsr_fuse_backward(B, N, H * W, C, L.tensor_desc(w, C, img_stride=img),
+                                       L.tensor_desc(f, C, img_stride=img, fmap=(1, N, 0, 1)),
+                                       L.tensor_desc(f, C, img_stride=img, fmap=(N - 1, N, 1, 1)),
+                                       L.tensor_desc(fu, C, img_stride=img), L.tensor_desc(dfu, C, img_stride=img),
+                                       L.tensor_desc(dl, C, img_stride=img),
+                                       L.tensor_desc(df, C, img_stride=img, fmap=(1, N, 0, 1)),
+                                       L.tensor_desc(df, C, img_stride=img, fmap=(N - 1, N, 1, 1)),
+                                       L.stream_ptr(all_feat.device)), 'dbsr_fuse_backward')
+    back = lambda t: t.view(B, N, H, W, C).permute(0, 1, 4, 2, 3).contiguous()        # noqa: E731
+    return back(dl), back(df)
+
+
+def warp_backward(dout, flow):
+    """dL/dfeat of warp(feat, flow) (warp.py:19-46): dout [N,C,H,W], flow [N,2,H,W] -> fp32 [N,C,H,W]."""
+    _need_cuda(dout, flow)
+    N, C, H, W = dout.shape
+    d = dout.permute(0, 2, 3, 1).contiguous()
+    fl = flow.to(torch.float32).contiguous()
+    out = torch.zeros(N, H, W, C, dtype=torch.float32, device=dout.device)
+    L.check(L.lib().dbsr_warp_backward(N, H, W, C, L.tensor_desc(d, C), fl.data_ptr(), 2 * H * W, out.data_ptr(),
+                                       L.FrameMap(1, 1, 0, 1), H * W * C, L.stream_ptr(dout.device)),
+            'dbsr_warp_backward')
+    return out.permute(0, 3, 1, 2).contiguous()

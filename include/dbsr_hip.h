@@ -83,6 +83,9 @@ typedef struct dbsr_conv_desc {
     int precise;                      /* 1: bf16 activations x fp32-packed weights on fp32 MFMA (fp32 out) */
     int max_blocks;                   /* > 0: cap on the persistent kernel's workgroups (CUs it occupies),
                                          leaving the rest of the chip to concurrent streams; 0 = all CUs */
+    dbsr_tensor gate;                 /* gate.ptr != NULL: out = (gate > 0) ? out : 0 after the residual --
+                                         the ReLU backward of the layer that produced the conv's input
+                                         (training dgrad); NHWC, output dtype; not with shuffle/NCHW out */
 } dbsr_conv_desc;
 
 /* Packed weight layout: [cout_pad][kgp*8] with k-group kg = (ky*kw+kx)*(cinp/8) + c/8, where
@@ -184,6 +187,54 @@ int dbsr_merge_prep(int B, int N, int hw, int c, dbsr_tensor proj, dbsr_tensor o
  * writes first/flow/feat into out channels [c0+81, c0+81+C+4). first: map pair->ref frame. */
 int dbsr_pwc_assemble(int n_pairs, int h, int w, int c, dbsr_tensor first, dbsr_tensor flow,
                       dbsr_tensor feat, dbsr_tensor out, void* stream);
+
+/* ---------------- training step (BASELINE configs[3]; trainers/simple_trainer.py:78-81) ----------------
+ * Backward of the DBSR part (PWC-Net is frozen, encoders.py:56-61).  Conv dgrad = dbsr_conv2d with the
+ * weights of dbsr_dgrad_weights (W'[ci][co][ky][kx] = W[co][ci][kh-1-ky][kw-1-kx]) packed as a normal
+ * conv, and the gate / residual epilogue for the ReLU / ResBlock backward (blocks.py:81-96). */
+
+/* Conv weight gradient, k = 1 or 3 (stride 1, pad k/2): dw[co][ci][ky][kx] (fp32, torch layout) =
+ * sum_p dy[p][co] * x[p + (ky-1, kx-1)][ci]; accumulate != 0 adds to dw.  x / dy: NHWC slices of the
+ * same dtype (cin / cout channels, ld and c0 multiples of 16 B, channels up to the next 16 B finite).
+ * Deterministic: fp32 partials per block (workspace) summed in a fixed order. */
+size_t dbsr_conv_wgrad_workspace_bytes(int n_frames, int h, int w, int cin, int cout, int k);
+int dbsr_conv_wgrad(int n_frames, int h, int w, dbsr_tensor x, int cin, dbsr_tensor dy, int cout, int k,
+                    float* dw, int accumulate, void* workspace, size_t workspace_bytes, void* stream);
+/* out[c] (+)= sum over the n*hw pixels of t[.][c] (conv bias gradient), fp32; deterministic. */
+size_t dbsr_chan_sum_workspace_bytes(int n, int hw, int c);
+int dbsr_chan_sum(int n, int hw, int c, dbsr_tensor t, float* out, int accumulate, void* workspace,
+                  size_t workspace_bytes, void* stream);
+/* L1 loss of pred vs gt (fp32 NCHW [B][C][H][W]) with boundary_ignore (image_quality_v2.py:24-66) into
+ * *loss (device), and its gradient through the predictor ReLU: dpre (NHWC, C channels) = [pred > 0] *
+ * sign(pred - gt) / count inside the crop, 0 outside.  workspace: >= ceil(B*H*W/256) floats. */
+int dbsr_l1_loss_backward(int B, int C, int H, int W, int boundary_ignore, const float* pred, const float* gt,
+                          dbsr_tensor dpre, float* loss, void* workspace, size_t workspace_bytes, void* stream);
+/* PixelShuffle(s) + ReLU backward (upsampling.py:51-58): du[b][y][x][c*s*s + i*s + j] =
+ * ds[b][y*s+i][x*s+j][c] * [gate > 0] (gate = the upsampler's forward output). */
+int dbsr_unshuffle_gate(int B, int H, int W, int s, int c, dbsr_tensor ds, dbsr_tensor gate, dbsr_tensor du,
+                        void* stream);
+/* Softmax-fusion backward (merging.py:116-124), addressing as dbsr_fuse_softmax: dref / doth = w * dfused,
+ * dlogits = w * dfused * (f - fused); weights = the forward's normalised weights. */
+int dbsr_fuse_backward(int B, int N, int hw, int c, dbsr_tensor weights, dbsr_tensor ref, dbsr_tensor oth,
+                       dbsr_tensor fused, dbsr_tensor dfused, dbsr_tensor dlogits, dbsr_tensor dref,
+                       dbsr_tensor doth, void* stream);
+/* merge-prep backward (merging.py:79-89) + the projection ReLU: dwp channels [0,c) = d base, [c,2c) = d diff
+ * of images b*N+n -> dproj = [proj > 0] * (n == 0 ? sum_n dbase - sum_{n>=1} ddiff : ddiff). */
+int dbsr_merge_prep_backward(int B, int N, int hw, int c, dbsr_tensor dwp, dbsr_tensor proj, dbsr_tensor dproj,
+                             void* stream);
+/* warp backward w.r.t. the features (warp.py:19-46): dfeat32[fmap(p)] += bilinear scatter of dout[p]
+ * (fp32 atomics; dfeat32 images dfeat_img_stride floats apart, pixels c floats apart). */
+int dbsr_warp_backward(int n, int h, int w, int c, dbsr_tensor dout, const float* flow, long long flow_img_stride,
+                       float* dfeat32, dbsr_frame_map fmap, long long dfeat_img_stride, void* stream);
+/* encoder output gradient (encoders.py:66-80): de[b*N+n] = [e > 0] * (n == 0 ? dref[b] : dsrc32[b*N+n]). */
+int dbsr_enc_grad_gate(int B, int N, int hw, int c, dbsr_tensor dref, const float* dsrc32, dbsr_tensor e,
+                       dbsr_tensor de, void* stream);
+/* torch.optim.Adam step (weight_decay 0) on flat fp32 buffers; grad is scaled by grad_scale first. */
+int dbsr_adam_step(long long n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq, float lr,
+                   float beta1, float beta2, float eps, int step, float grad_scale, void* stream);
+/* wt[ci][co][ky][kx] = w[co][ci][kh-1-ky][kw-1-kx] (fp32): the dgrad conv's weights, to pack with
+ * dbsr_conv_pack_weights(cout = cin, cin = cout). */
+int dbsr_dgrad_weights(const float* w, int cout, int cin, int kh, int kw, float* wt, void* stream);
 
 /* Fill an NHWC slice with zeros (used for channel padding of persistent buffers). */
 int dbsr_zero(void* ptr, size_t bytes, void* stream);

@@ -1,0 +1,182 @@
+"""Training step (BASELINE configs[3]) on the HIP kernels: op-level backward parity against torch autograd
+of the same ops, and whole-step gradients / Adam update against torch autograd of the oracle forward
+(the reference's training step: L1(pred, gt, boundary_ignore=40).backward(), Adam(lr=1e-4);
+trainers/simple_trainer.py:78-81, actors/dbsr_actors.py:27-47, default_synthetic.py:85-96).
+
+Tolerances: fp32 kernels vs torch fp32 -- 1e-4 relative to the gradient's max magnitude (different
+summation orders over up to 10^5 pixels); bf16 kernels vs torch on the same bf16-rounded operands --
+2e-2 relative.  Whole network: the gradients of the early weight-predictor / offset-feature layers
+sit behind ReLU gates that flip on rounding-level forward differences (the oracle's own fp32 vs fp64
+gradients differ by 6.5e-4 of the max at weight_predictor.1.conv2), so fp32 is held to the loss within
+1e-5, per-tensor cosine similarity >= 1 - 1e-4 and max-rel <= 2e-2; bf16 to the loss within 1 % and
+cosine similarity >= 0.97 per tensor."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+@pytest.fixture(scope='module')
+def ops():
+    from dbsr_amd import ops as O
+    return O
+
+
+def _rel(a, b):
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-12))
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('case', [(2, 64, 20, 36, 64, 3), (1, 4, 9, 17, 64, 3), (2, 512, 8, 16, 64, 1),
+                                  (1, 32, 24, 40, 3, 1), (1, 128, 12, 12, 512, 3), (2, 192, 16, 16, 128, 3)])
+def test_conv_wgrad(ops, dtype, case):
+    N, Cin, H, W, Cout, k = case
+    gen = torch.Generator().manual_seed(Cin + Cout * 3 + H)
+    x = torch.randn(N, Cin, H, W, generator=gen)
+    dy = torch.randn(N, Cout, H, W, generator=gen)
+    xr, dyr = x.to(dtype).float(), dy.to(dtype).float()
+    w = torch.zeros(Cout, Cin, k, k, requires_grad=True)
+    F.conv2d(xr, w, padding=k // 2).backward(dyr)
+    out = ops.conv2d_wgrad(x.to(DEV), dy.to(DEV), k, compute_dtype=dtype).cpu()
+    assert _rel(out, w.grad) <= 1e-4
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('case', [(2, 64, 20, 36, 64, 3), (1, 64, 12, 16, 4, 3), (2, 64, 8, 16, 512, 1),
+                                  (1, 3, 24, 40, 32, 1), (1, 512, 12, 12, 64, 3)])
+def test_conv_dgrad_gate_residual(ops, dtype, case):
+    """dX of a conv (dgrad-packed weights on the forward kernel) + residual, gated by a ReLU output."""
+    N, Cout, H, W, Cin, k = case
+    gen = torch.Generator().manual_seed(Cin * 5 + Cout + W)
+    dy = torch.randn(N, Cout, H, W, generator=gen)
+    w = torch.randn(Cout, Cin, k, k, generator=gen) / (Cin * k * k) ** 0.5
+    res = torch.randn(N, Cin, H, W, generator=gen)
+    gate = F.relu(torch.randn(N, Cin, H, W, generator=gen))
+    dyr, wr, rr = (t.to(dtype).float() for t in (dy, w, res))
+    x = torch.zeros(N, Cin, H, W, requires_grad=True)
+    F.conv2d(x, wr, padding=k // 2).backward(dyr)
+    ref = (x.grad + rr) * (gate > 0)
+    out = ops.conv2d_dgrad(dy.to(DEV), w.to(DEV), residual=res.to(DEV), gate=gate.to(DEV),
+                           compute_dtype=dtype).float().cpu()
+    tol = 1e-4 if dtype == torch.float32 else 2e-2
+    assert _rel(out, ref) <= tol
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+def test_fuse_backward(ops, dtype):
+    gen = torch.Generator().manual_seed(3)
+    B, N, C, H, W = 2, 5, 64, 6, 7
+    lg = torch.randn(B, N, C, H, W, generator=gen)
+    f = torch.randn(B, N, C, H, W, generator=gen)
+    df = torch.randn(B, C, H, W, generator=gen)
+    lgr, fr = lg.to(dtype).float().requires_grad_(), f.to(dtype).float().requires_grad_()
+    w = F.softmax(lgr, dim=1)
+    fused = (fr * w).sum(dim=1)
+    fused.backward(df.to(dtype).float())
+    dl, dfe = ops.fuse_backward(w.detach().to(DEV).to(dtype), f.to(DEV).to(dtype), fused.detach().to(DEV).to(dtype),
+                                df.to(DEV).to(dtype))
+    tol = 1e-5 if dtype == torch.float32 else 3e-2
+    assert _rel(dl.float().cpu(), lgr.grad) <= tol
+    assert _rel(dfe.float().cpu(), fr.grad) <= tol
+
+
+def test_warp_backward(ops):
+    from oracle import dbsr_oracle as orc
+    gen = torch.Generator().manual_seed(4)
+    x = torch.randn(3, 16, 12, 20, generator=gen, requires_grad=True)
+    fl = torch.randn(3, 2, 12, 20, generator=gen) * 3.0
+    dy = torch.randn(3, 16, 12, 20, generator=gen)
+    orc.warp(x, fl).backward(dy)
+    out = ops.warp_backward(dy.to(DEV), fl.to(DEV)).cpu()
+    assert _rel(out, x.grad) <= 1e-5
+
+
+# ----------------------------------------------------------------------------------------------------
+# whole training step
+# ----------------------------------------------------------------------------------------------------
+def _oracle_grads(sd_t, burst, gt, bi):
+    from oracle import dbsr_oracle as orc
+    sd = {k: v.clone().requires_grad_(not k.startswith('encoder.alignment_net')) for k, v in sd_t.items()}
+    pred, _ = orc.dbsr_forward(burst, sd)
+    loss = F.l1_loss(pred[..., bi:-bi, bi:-bi], gt[..., bi:-bi, bi:-bi])
+    loss.backward()
+    return float(loss), {k: v.grad for k, v in sd.items() if v.grad is not None}
+
+
+def _trainer(synth_sd, dtype):
+    import dbsr_amd
+    from dbsr_amd.training import DBSRTrainer
+    net = dbsr_amd.dbsrnet_cvpr2021(**dbsr_amd.DBSR_SYNTHETIC_KWARGS)
+    net.load_state_dict(synth_sd)
+    net = net.to(DEV).set_compute_dtype(dtype)
+    return net, DBSRTrainer(net, boundary_ignore=40)
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+def test_train_step_grads_vs_oracle(synth_sd, dtype):
+    from dbsr_amd.burst import synthetic_bursts
+    burst, gt = synthetic_bursts(2, 3, 24, 32, sr_factor=8, seed=17)
+    ref_loss, ref_g = _oracle_grads(synth_sd, burst, gt, 40)
+    net, tr = _trainer(synth_sd, dtype)
+    loss, _ = tr.forward_backward(burst.to(DEV), gt.to(DEV))
+    torch.cuda.synchronize()
+    mine = {k: v.cpu() for k, v in tr.grads().items()}
+    assert set(mine) == set(ref_g), set(mine) ^ set(ref_g)
+    print('loss', float(loss), ref_loss)
+    gmax = max(float(g.abs().max()) for g in ref_g.values())
+    rel, cos = [], []
+    for k, g in ref_g.items():
+        if k == 'merging.weight_predictor.4.0.bias':
+            # the last logit conv's bias is shared by all N frames of the softmax: its exact gradient is 0
+            # (softmax shift invariance, merging.py:117); both sides are rounding noise
+            assert float(mine[k].abs().max()) <= 1e-4 * gmax
+            continue
+        rel.append((_rel(mine[k], g), k))
+        cos.append((1 - float(F.cosine_similarity(mine[k].double().flatten(), g.double().flatten(), dim=0)), k))
+    rel.sort(reverse=True)
+    cos.sort(reverse=True)
+    print('max-rel worst', rel[:4])
+    print('1-cos worst', cos[:4])
+    if dtype == torch.float32:
+        assert abs(float(loss) - ref_loss) <= 1e-5 * max(1.0, abs(ref_loss))
+        assert rel[0][0] <= 2e-2, rel[:3]
+        assert cos[0][0] <= 1e-4, cos[:3]
+    else:
+        assert abs(float(loss) - ref_loss) <= 1e-2 * abs(ref_loss)
+        assert cos[0][0] <= 3e-2, cos[:3]
+
+
+def test_train_step_adam_update_fp32(synth_sd):
+    """One step updates the parameters exactly as torch.optim.Adam(lr=1e-4) does with that step's
+    gradients (the gradients themselves are checked against the oracle above)."""
+    from dbsr_amd.burst import synthetic_bursts
+    burst, gt = synthetic_bursts(1, 3, 24, 32, sr_factor=8, seed=18)
+    net, tr = _trainer(synth_sd, torch.float32)
+    before = {k: v.detach().clone() for k, v in net.named_parameters() if not k.startswith('encoder.alignment_net')}
+    tr.step(burst.to(DEV), gt.to(DEV))
+    torch.cuda.synchronize()
+    grads = tr.grads()
+    params = {k: before[k].clone().requires_grad_() for k in before}
+    opt = torch.optim.Adam(list(params.values()), lr=1e-4)
+    for k, p in params.items():
+        p.grad = grads[k].clone()
+    opt.step()
+    cur = dict(net.named_parameters())
+    for k, p in params.items():
+        np.testing.assert_allclose(cur[k].detach().cpu().numpy(), p.detach().cpu().numpy(), rtol=1e-6, atol=1e-7)
+
+
+def test_cfg4_training_steps_bf16(synth_sd):
+    """configs[3]'s step shape (SyntheticBurst 14 frames, 128x128 -> 1024x1024, bf16; batch 2 here to
+    keep the test short): three Adam steps on one batch run, stay finite and lower the loss."""
+    from dbsr_amd.burst import synthetic_bursts
+    burst, gt = synthetic_bursts(2, 14, 128, 128, sr_factor=8, seed=19)
+    net, tr = _trainer(synth_sd, torch.bfloat16)
+    b, g = burst.to(DEV), gt.to(DEV)
+    losses = [float(tr.step(b, g)) for _ in range(3)]
+    print('losses', losses)
+    assert all(np.isfinite(losses))
+    assert losses[-1] < losses[0]

@@ -126,3 +126,58 @@ def test_gloo_world2_frame_sharded_fusion():
     for p in procs:
         p.join(timeout=60)
     assert res[0][1] <= 1e-4, res            # sharded == unsharded forward (fp32, rounding order only)
+
+
+def _ddp_worker(rank, world, port, q):
+    """Data-parallel training gradient (configs[3]): each rank differentiates the oracle forward on its
+    shard of the global batch (stand-in for the HIP step, which needs a GPU), flattens the gradients in
+    the trainer's layout and averages them with the trainer's bucketed all-reduce."""
+    import torch.distributed as dist
+    import torch.nn.functional as F
+    import dbsr_amd
+    from dbsr_amd import parallel, training
+    from dbsr_amd.burst import synthetic_bursts
+    from oracle import dbsr_oracle as orc
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        torch.set_num_threads(2)
+        net = dbsr_amd.build_synthetic_net(seed=0)
+        layout, buckets = training.flat_layout(net)
+        sd0 = {k: v.detach().clone() for k, v in net.state_dict().items()}
+        burst, gt = synthetic_bursts(4, 3, 16, 16, sr_factor=8, seed=5)
+
+        def grads(b, g):
+            sd = {k: v.clone().requires_grad_(not k.startswith('encoder.alignment_net')) for k, v in sd0.items()}
+            pred, _ = orc.dbsr_forward(b, sd)
+            F.l1_loss(pred[..., 40:-40, 40:-40], g[..., 40:-40, 40:-40]).backward()
+            return torch.cat([sd[n].grad.reshape(-1) for n, _ in layout])
+
+        a, b = parallel.shard_range(burst.shape[0], rank, world)
+        flat = grads(burst[a:b], gt[a:b])
+        works = [training.allreduce_bucket(flat, lo, hi) for lo, hi in buckets]
+        for w in works:
+            w.wait()
+        flat /= world
+        full = grads(burst, gt)
+        q.put((rank, float((flat - full).abs().max() / full.abs().max()), buckets[-1][1] == flat.numel()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_ddp_gradients_equal_single_process():
+    """the all-reduced sharded gradients equal a single-process step on the
+    concatenated batch (L1 mean over equal shards; fp32 summation-order tolerance)."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ddp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    for rank, err, covers in res:
+        assert covers                      # the three buckets cover every trainable parameter
+        assert err <= 1e-5, (rank, err)
