@@ -12,7 +12,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('DBSR_HIP_LIB', os.path.join(_HERE, 'libdbsr_hip.so'))
 
-DBSR_F32, DBSR_BF16 = 0, 1
+DBSR_F32, DBSR_BF16, DBSR_F16 = 0, 1, 2
 ACT_NONE, ACT_RELU, ACT_LRELU = 0, 1, 2
 OUT_NHWC, OUT_SHUFFLE, OUT_NCHW_F32 = 0, 1, 2
 ABI_VERSION = 7
@@ -139,6 +139,8 @@ def dtype_code(dt):
         return DBSR_F32
     if dt == torch.bfloat16:
         return DBSR_BF16
+    if dt == torch.float16:
+        return DBSR_F16
     raise ValueError('unsupported dtype %s' % dt)
 
 

@@ -6,8 +6,9 @@
 
 namespace dbsr {
 
-typedef uint16_t bf16_t;                                            // storage type
-typedef __attribute__((ext_vector_type(8))) short bf16x8_t;        // MFMA bf16 operand (8 elems)
+typedef uint16_t bf16_t;                                            // bf16 storage type
+typedef _Float16 f16_t;                                             // fp16 storage type (configs[4])
+typedef __attribute__((ext_vector_type(8))) short bf16x8_t;        // MFMA 16-bit operand (8 elems, raw bits)
 typedef __attribute__((ext_vector_type(4))) float f32x4_t;          // 16x16 MFMA accumulator
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
 
@@ -31,11 +32,32 @@ __device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {
     return __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2_t{lo, hi}, bf16x2_t));
 }
 __device__ __forceinline__ bf16_t f2bf(float f) { return __builtin_bit_cast(unsigned short, (__bf16)f); }
+typedef __attribute__((ext_vector_type(2))) _Float16 f16x2_t;
+
+// Two 16-bit values per dword (bf16 or fp16 storage): unpack to fp32 / pack from fp32 (round to nearest
+// even, hardware v_cvt_pk_* conversions)
+template <typename T> struct H16;
+template <> struct H16<bf16_t> {
+    static __device__ __forceinline__ float lo(unsigned u) { return __uint_as_float(u << 16); }
+    static __device__ __forceinline__ float hi(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
+    static __device__ __forceinline__ unsigned pack(float a, float b) { return pack_bf16x2(a, b); }
+};
+template <> struct H16<f16_t> {
+    static __device__ __forceinline__ float lo(unsigned u) { return (float)__builtin_bit_cast(f16x2_t, u)[0]; }
+    static __device__ __forceinline__ float hi(unsigned u) { return (float)__builtin_bit_cast(f16x2_t, u)[1]; }
+    static __device__ __forceinline__ unsigned pack(float a, float b) {
+        return __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2_t{a, b}, f16x2_t));
+    }
+};
 
 template <typename T> struct elem;
 template <> struct elem<float> {
     static __device__ __forceinline__ float ld(const float* p) { return *p; }
     static __device__ __forceinline__ void st(float* p, float v) { *p = v; }
+};
+template <> struct elem<f16_t> {
+    static __device__ __forceinline__ float ld(const f16_t* p) { return (float)*p; }
+    static __device__ __forceinline__ void st(f16_t* p, float v) { *p = (f16_t)v; }
 };
 template <> struct elem<bf16_t> {
     static __device__ __forceinline__ float ld(const bf16_t* p) { return bf2f(*p); }
@@ -47,22 +69,24 @@ __device__ __forceinline__ void load8(const float* p, float (&v)[8]) {
     float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
     v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
-__device__ __forceinline__ void load8(const bf16_t* p, float (&v)[8]) {
+template <typename T>
+__device__ __forceinline__ void load8(const T* p, float (&v)[8]) {      // 16-bit storage (bf16 / fp16)
     u32x4_t q = *(const u32x4_t*)p;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        v[2 * i] = __uint_as_float(q[i] << 16);
-        v[2 * i + 1] = __uint_as_float(q[i] & 0xffff0000u);
+        v[2 * i] = H16<T>::lo(q[i]);
+        v[2 * i + 1] = H16<T>::hi(q[i]);
     }
 }
 __device__ __forceinline__ void store8(float* p, const float (&v)[8]) {
     *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
     *(float4*)(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
 }
-__device__ __forceinline__ void store8(bf16_t* p, const float (&v)[8]) {
+template <typename T>
+__device__ __forceinline__ void store8(T* p, const float (&v)[8]) {     // 16-bit storage (bf16 / fp16)
     u32x4_t q;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) q[i] = pack_bf16x2(v[2 * i], v[2 * i + 1]);
+    for (int i = 0; i < 4; ++i) q[i] = H16<T>::pack(v[2 * i], v[2 * i + 1]);
     *(u32x4_t*)p = q;
 }
 

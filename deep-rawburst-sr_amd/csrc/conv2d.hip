@@ -30,7 +30,9 @@ inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
 // conv with cin > 16 is a whole number of 32-channel MFMA chunks per tap
 inline int cin_pad(int cin) { return cin <= 16 ? round_up(cin, 8) : round_up(cin, 32); }
 
-int g_tiled_enabled = 1;   // dbsr_set_conv_algo: 0 generic only, 1 LDS-tiled where applicable, 2 + pipelined
+int g_tiled_enabled = 1;
+inline bool is16(int dtype) { return dtype == DBSR_BF16 || dtype == DBSR_F16; }   // 16-bit activations
+inline int esize(int dtype) { return is16(dtype) ? 2 : 4; }   // dbsr_set_conv_algo: 0 generic only, 1 LDS-tiled where applicable, 2 + pipelined
 
 struct ConvK {
     const void* x; long long x_is; int x_ld; dbsr_frame_map xm; int in_h, in_w;
@@ -59,6 +61,11 @@ template <> struct Frag<bf16_t> {
     __device__ __forceinline__ void load(const bf16_t* p) { v = *(const bf16x8_t*)p; }
     __device__ __forceinline__ void zero() { v = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0}; }
 };
+template <> struct Frag<f16_t> {
+    bf16x8_t v;                                                 // raw fp16 bits
+    __device__ __forceinline__ void load(const f16_t* p) { v = *(const bf16x8_t*)p; }
+    __device__ __forceinline__ void zero() { v = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0}; }
+};
 template <> struct Frag<float> {
     float4 a, b;
     __device__ __forceinline__ void load(const float* p) { a = *(const float4*)p; b = *(const float4*)(p + 4); }
@@ -69,6 +76,11 @@ template <> struct Frag<float> {
         b = make_float4(__uint_as_float(q[2] << 16), __uint_as_float(q[2] & 0xffff0000u),
                         __uint_as_float(q[3] << 16), __uint_as_float(q[3] & 0xffff0000u));
     }
+    __device__ __forceinline__ void load(const f16_t* p) {       // fp16 activations, fp32 ("precise") math
+        const u32x4_t q = *(const u32x4_t*)p;
+        a = make_float4(H16<f16_t>::lo(q[0]), H16<f16_t>::hi(q[0]), H16<f16_t>::lo(q[1]), H16<f16_t>::hi(q[1]));
+        b = make_float4(H16<f16_t>::lo(q[2]), H16<f16_t>::hi(q[2]), H16<f16_t>::lo(q[3]), H16<f16_t>::hi(q[3]));
+    }
     __device__ __forceinline__ void zero() { a = make_float4(0, 0, 0, 0); b = a; }
 };
 
@@ -76,6 +88,10 @@ __device__ __forceinline__ f32x4_t mma(const Frag<bf16_t>& A, const Frag<bf16_t>
     typedef __attribute__((ext_vector_type(8))) __bf16 bfv;
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bfv, A.v), __builtin_bit_cast(bfv, B.v), c,
                                                    0, 0, 0);
+}
+__device__ __forceinline__ f32x4_t mma(const Frag<f16_t>& A, const Frag<f16_t>& B, f32x4_t c) {
+    typedef __attribute__((ext_vector_type(8))) _Float16 hv;
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(hv, A.v), __builtin_bit_cast(hv, B.v), c, 0, 0, 0);
 }
 __device__ __forceinline__ f32x4_t mma(const Frag<float>& A, const Frag<float>& B, f32x4_t c) {
     c = __builtin_amdgcn_mfma_f32_16x16x4f32(A.a.x, B.a.x, c, 0, 0, 0);
@@ -117,8 +133,8 @@ __device__ __forceinline__ void store4(const ConvK& k, long long off, const floa
         if (nvalid == 4 && k.vec_store) {
             if constexpr (sizeof(T) == 2) {
                 uint2 q;
-                q.x = pack_bf16x2(v[0], v[1]);
-                q.y = pack_bf16x2(v[2], v[3]);
+                q.x = H16<T>::pack(v[0], v[1]);
+                q.y = H16<T>::pack(v[2], v[3]);
                 *(uint2*)y = q;
             } else {
                 *(float4*)y = make_float4(v[0], v[1], v[2], v[3]);
@@ -257,15 +273,15 @@ __global__ __launch_bounds__(256) void conv2d_kernel(ConvK k) {
             constexpr int PITCH = MT * 16 + 8;                     // bf16 per LDS row (+16 B: spreads banks)
             constexpr int LPR = MT * 2;                            // lanes per pixel row (16 B each)
             constexpr int RPI = 64 / LPR;                          // rows per store instruction
-            __shared__ __attribute__((aligned(16))) bf16_t stile[4][NT * 16 * PITCH];
-            bf16_t* st = stile[wave];
+            __shared__ __attribute__((aligned(16))) uint16_t stile[4][NT * 16 * PITCH];
+            uint16_t* st = stile[wave];
 #pragma unroll
             for (int j = 0; j < NT; ++j)
 #pragma unroll
                 for (int i = 0; i < MT; ++i) {
                     uint2 q;
-                    q.x = pack_bf16x2(apply_act(acc[i][j][0] + bias[i][0], k.act), apply_act(acc[i][j][1] + bias[i][1], k.act));
-                    q.y = pack_bf16x2(apply_act(acc[i][j][2] + bias[i][2], k.act), apply_act(acc[i][j][3] + bias[i][3], k.act));
+                    q.x = H16<T>::pack(apply_act(acc[i][j][0] + bias[i][0], k.act), apply_act(acc[i][j][1] + bias[i][1], k.act));
+                    q.y = H16<T>::pack(apply_act(acc[i][j][2] + bias[i][2], k.act), apply_act(acc[i][j][3] + bias[i][3], k.act));
                     *(uint2*)(st + (j * 16 + col) * PITCH + i * 16 + kgl * 4) = q;
                 }
             __syncthreads();
@@ -336,7 +352,7 @@ __global__ void pack_weights_pipe_kernel(const bf16_t* __restrict__ rows, int CG
 }
 
 __global__ void pack_weights_kernel(const float* __restrict__ w, const float* __restrict__ bias, int cout, int cin,
-                                    int kh, int kw, int CG, int KG, int Kp, int cout_pad, int shuffle, int is_bf16,
+                                    int kh, int kw, int CG, int KG, int Kp, int cout_pad, int shuffle, int dtype,
                                     void* __restrict__ out, float* __restrict__ bias_out) {
     const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     const long long total = (long long)cout_pad * Kp;
@@ -357,8 +373,10 @@ __global__ void pack_weights_kernel(const float* __restrict__ w, const float* __
             v = w[(((long long)co_src * cin + c) * kh + ky) * kw + kx];
         }
     }
-    if (is_bf16)
+    if (dtype == DBSR_BF16)
         ((bf16_t*)out)[idx] = f2bf(v);
+    else if (dtype == DBSR_F16)
+        ((f16_t*)out)[idx] = (f16_t)v;
     else
         ((float*)out)[idx] = v;
     if (bias_out && kk == 0 && co < cout) bias_out[co] = bias ? bias[co_src] : 0.f;
@@ -567,8 +585,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_tiled_kernel(ConvK k, int tile
                 for (int r = 0; r < 4; ++r) v[r] = apply_act(acc[i][j][r] + bias[i][r], k.act);
                 if constexpr (sizeof(T) == 2) {
                     uint2 q;
-                    q.x = pack_bf16x2(v[0], v[1]);
-                    q.y = pack_bf16x2(v[2], v[3]);
+                    q.x = H16<T>::pack(v[0], v[1]);
+                    q.y = H16<T>::pack(v[2], v[3]);
                     *(uint2*)(ob + pix * C::OSTR + co * 2) = q;
                 } else {
                     *(float4*)(ob + pix * C::OSTR + co * 4) = make_float4(v[0], v[1], v[2], v[3]);
@@ -612,9 +630,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_tiled_kernel(ConvK k, int tile
                 if constexpr (sizeof(T) == 2) {
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
-                        const float lo = __uint_as_float(val[q] << 16) + __uint_as_float(rv[e][q] << 16);
-                        const float hi = __uint_as_float(val[q] & 0xffff0000u) + __uint_as_float(rv[e][q] & 0xffff0000u);
-                        val[q] = pack_bf16x2(apply_act(lo, k.post_act), apply_act(hi, k.post_act));
+                        const float lo = H16<T>::lo(val[q]) + H16<T>::lo(rv[e][q]);
+                        const float hi = H16<T>::hi(val[q]) + H16<T>::hi(rv[e][q]);
+                        val[q] = H16<T>::pack(apply_act(lo, k.post_act), apply_act(hi, k.post_act));
                     }
                 } else {
 #pragma unroll
@@ -628,8 +646,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_tiled_kernel(ConvK k, int tile
                 if constexpr (sizeof(T) == 2) {
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
-                        const unsigned keep = (__uint_as_float(gv[q] << 16) > 0.f ? 0x0000ffffu : 0u) |
-                                              (__uint_as_float(gv[q] & 0xffff0000u) > 0.f ? 0xffff0000u : 0u);
+                        const unsigned keep = (H16<T>::lo(gv[q]) > 0.f ? 0x0000ffffu : 0u) |
+                                              (H16<T>::hi(gv[q]) > 0.f ? 0xffff0000u : 0u);
                         val[q] &= keep;
                     }
                 } else {
@@ -739,11 +757,10 @@ struct PipeCfg {
 // each of its four 16-lane groups, the 4 lanes with equal p mod 4 read 4 distinct phys values.
 __device__ __forceinline__ int halo_phys(int p, int g) { return 2 * (g & 1) + ((g >> 1) ^ ((p >> 2) & 1)); }
 
-template <int WM, int TW, int TH, int EPI>
+template <typename T, int WM, int TW, int TH, int EPI>
 __global__ __launch_bounds__(512, 1) void conv3x3_pipe_kernel(ConvK k, int tiles_x, int tiles_y, int nct,
                                                               int ntiles) {
     using C = PipeCfg<WM, TW, TH>;
-    typedef bf16_t T;
     DBSR_OWN_SIMDS();
     __shared__ __attribute__((aligned(16))) u32x4_t lds[C::LDS_U4];
     float* lbias = (float*)(lds + 2 * C::STAGE_U4);      // [nct * WM] fp32
@@ -871,8 +888,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pipe_kernel(ConvK k, int tiles
                 const u32x4_t rq = resv[q];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    v[2 * e] = act2(v[2 * e] + __uint_as_float(rq[e] << 16));
-                    v[2 * e + 1] = act2(v[2 * e + 1] + __uint_as_float(rq[e] & 0xffff0000u));
+                    v[2 * e] = act2(v[2 * e] + H16<T>::lo(rq[e]));
+                    v[2 * e + 1] = act2(v[2 * e + 1] + H16<T>::hi(rq[e]));
                 }
             }
             u32x4_t o;
@@ -896,7 +913,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pipe_kernel(ConvK k, int tiles
                 o[1] = o[2] = o[3] = 0u;
             } else {
 #pragma unroll
-                for (int e = 0; e < 4; ++e) o[e] = pack_bf16x2(v[2 * e], v[2 * e + 1]);
+                for (int e = 0; e < 4; ++e) o[e] = H16<T>::pack(v[2 * e], v[2 * e + 1]);
             }
             pend[q] = o;
             acc[2 * h][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
@@ -1006,7 +1023,7 @@ int num_cus() {
     return g_num_cus;
 }
 
-template <int WM, int TW, int TH>
+template <typename T, int WM, int TW, int TH>
 int launch_pipe(const ConvK& k, int n_frames, hipStream_t s) {
     const int tiles_x = (k.out_w + TW - 1) / TW, tiles_y = (k.out_h + TH - 1) / TH;
     const int nct = (k.cout + WM - 1) / WM;
@@ -1025,7 +1042,7 @@ int launch_pipe(const ConvK& k, int n_frames, hipStream_t s) {
     else if (k.r && k.act == DBSR_ACT_NONE && k.post_act == DBSR_ACT_RELU) epi = 2;
     else if (!k.r && k.act == DBSR_ACT_NONE) epi = 3;
 #define DBSR_PIPE_LAUNCH(E)                                                                                    \
-    hipLaunchKernelGGL((conv3x3_pipe_kernel<WM, TW, TH, E>), dim3(grid), dim3(512), 0, s, k, tiles_x, tiles_y, \
+    hipLaunchKernelGGL((conv3x3_pipe_kernel<T, WM, TW, TH, E>), dim3(grid), dim3(512), 0, s, k, tiles_x, tiles_y, \
                        nct, (int)nt)
     switch (epi) {
         case 4:
@@ -1045,8 +1062,8 @@ int launch_pipe(const ConvK& k, int n_frames, hipStream_t s) {
 // aligned NHWC bf16 output (staged epilogue), and enough tiles to fill the chip
 int g_pipe_enabled = 1;
 int pick_pipe(const dbsr_conv_desc* d) {
-    if (!g_pipe_enabled || d->x.dtype != DBSR_BF16 || d->precise || d->kh != 3 || d->kw != 3 || d->stride != 1 ||
-        d->pad != 1 || d->dil != 1 || d->cin <= 16 || d->out_mode != DBSR_OUT_NHWC || d->y.dtype != DBSR_BF16)
+    if (!g_pipe_enabled || !is16(d->x.dtype) || d->precise || d->kh != 3 || d->kw != 3 || d->stride != 1 ||
+        d->pad != 1 || d->dil != 1 || d->cin <= 16 || d->out_mode != DBSR_OUT_NHWC || d->y.dtype != d->x.dtype)
         return 0;
     if (d->y.ld % 8 || d->y.c0 % 8 || d->cout % 8 || (d->res.ptr && (d->res.ld % 8 || d->res.c0 % 8))) return 0;
     if (d->gate.ptr) return 0;                                   // gated (backward) convs: tiled/generic kernels
@@ -1059,9 +1076,10 @@ int pick_pipe(const dbsr_conv_desc* d) {
     return (nt >= 256 || g_pipe_enabled == 2) ? cfg : 0;
 }
 
+template <typename T>
 int dispatch_pipe(int cfg, const ConvK& k, const dbsr_conv_desc* d, hipStream_t s) {
-    if (cfg == 1) return launch_pipe<64, 48, 8>(k, d->n_frames, s);
-    return launch_pipe<32, 64, 8>(k, d->n_frames, s);
+    if (cfg == 1) return launch_pipe<T, 64, 48, 8>(k, d->n_frames, s);
+    return launch_pipe<T, 32, 64, 8>(k, d->n_frames, s);
 }
 
 template <typename T, int MT, int NT, typename XT = T>
@@ -1121,7 +1139,7 @@ void pick_generic_tile(const ConvK& k, int& best_m, int& best_n) {
 // 3x3 'same' convolutions (pad == dilation) with dilation 1/2/4/8 (the PWC refiner's context
 // network, pwcnet.py:227-241, has 2/4/8; fp32 tiles with dilation 8 exceed the LDS)
 bool use_tiled(const dbsr_conv_desc* d) {
-    const bool bf = d->x.dtype == DBSR_BF16;
+    const bool bf = is16(d->x.dtype);
     const bool dil_ok = (d->dil == 1 || d->dil == 2 || d->dil == 4 || (d->dil == 8 && bf)) && d->pad == d->dil;
     return !d->precise && cin_pad(d->cin) * (bf ? 2 : 4) + 64 <= ZERO_PAGE_BYTES && d->kh == 3 && d->kw == 3 &&
            d->stride == 1 && dil_ok && d->cin > 16 && d->out_h >= 8 && d->out_w >= 8 &&
@@ -1166,7 +1184,7 @@ template <typename T>
 int dispatch_conv(const ConvK& k, const dbsr_conv_desc* d, hipStream_t s) {
     if constexpr (sizeof(T) == 2) {
         const int cfg = pick_pipe(d);
-        if (cfg) return dispatch_pipe(cfg, k, d, s);
+        if (cfg) return dispatch_pipe<T>(cfg, k, d, s);
     }
     if (use_tiled(d)) {
         switch (d->dil) {
@@ -1203,13 +1221,13 @@ int dispatch_conv(const ConvK& k, const dbsr_conv_desc* d, hipStream_t s) {
 // (g, col) ends up with channels 8g..8g+7 of its pixel: one 16-B store per lane, 64 contiguous bytes
 // (the whole 32-channel output pixel) per 4 lanes.
 // ------------------------------------------------------------------------------------------------
-template <int PG, int KS>
+template <typename T, int PG, int KS>
 __global__ __launch_bounds__(512) void upsample_shuffle_kernel(ConvK k) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int g = lane >> 4, col = lane & 15;
     const int s = k.shuffle, s2 = s * s;
     const int hw = k.out_h * k.out_w;
-    Frag<bf16_t> b[PG][KS];
+    Frag<T> b[PG][KS];
     int pf[PG], py[PG], px[PG];
 #pragma unroll
     for (int j = 0; j < PG; ++j) {
@@ -1219,7 +1237,7 @@ __global__ __launch_bounds__(512) void upsample_shuffle_kernel(ConvK k) {
         pf[j] = ok ? f : -1;
         py[j] = rr / k.out_w;
         px[j] = rr - py[j] * k.out_w;
-        const bf16_t* xp = (const bf16_t*)k.x + map_frame(k.xm, f) * k.x_is + (long long)rr * k.x_ld + g * 8;
+        const T* xp = (const T*)k.x + map_frame(k.xm, f) * k.x_is + (long long)rr * k.x_ld + g * 8;
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
             if (ok) b[j][ks].load(xp + ks * 32);
@@ -1227,14 +1245,14 @@ __global__ __launch_bounds__(512) void upsample_shuffle_kernel(ConvK k) {
         }
     }
     const int m_row = 8 * (col >> 2) + (col & 3);           // + 4h: packed row within the sub-pixel's 32
-    auto load_a = [&](int sub, Frag<bf16_t> (&a)[2][KS]) {
+    auto load_a = [&](int sub, Frag<T> (&a)[2][KS]) {
 #pragma unroll
         for (int h = 0; h < 2; ++h)
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks)
-                a[h][ks].load((const bf16_t*)k.w + (long long)(sub * 32 + m_row + 4 * h) * k.Kp + ks * 32 + g * 8);
+                a[h][ks].load((const T*)k.w + (long long)(sub * 32 + m_row + 4 * h) * k.Kp + ks * 32 + g * 8);
     };
-    Frag<bf16_t> a_cur[2][KS], a_nxt[2][KS];
+    Frag<T> a_cur[2][KS], a_nxt[2][KS];
     int sub = wave;
     if (sub < s2) load_a(sub, a_cur);
     for (; sub < s2; sub += 8) {
@@ -1264,13 +1282,13 @@ __global__ __launch_bounds__(512) void upsample_shuffle_kernel(ConvK k) {
             u32x4_t o;
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
-                o[e] = pack_bf16x2(apply_act(acc[0][j][2 * e] + bv[2 * e], k.act),
+                o[e] = H16<T>::pack(apply_act(acc[0][j][2 * e] + bv[2 * e], k.act),
                                    apply_act(acc[0][j][2 * e + 1] + bv[2 * e + 1], k.act));
-                o[2 + e] = pack_bf16x2(apply_act(acc[1][j][2 * e] + bv[4 + 2 * e], k.act),
+                o[2 + e] = H16<T>::pack(apply_act(acc[1][j][2 * e] + bv[4 + 2 * e], k.act),
                                        apply_act(acc[1][j][2 * e + 1] + bv[4 + 2 * e + 1], k.act));
             }
             const long long Y = (long long)py[j] * s + sy, X = (long long)px[j] * s + sx;
-            *(u32x4_t*)((bf16_t*)k.y + map_frame(k.ym, pf[j]) * k.y_is + (Y * (k.out_w * s) + X) * k.y_ld + k.y_c0 +
+            *(u32x4_t*)((T*)k.y + map_frame(k.ym, pf[j]) * k.y_is + (Y * (k.out_w * s) + X) * k.y_ld + k.y_c0 +
                         8 * g) = o;
         }
         if (sub + 8 < s2) {
@@ -1283,18 +1301,19 @@ __global__ __launch_bounds__(512) void upsample_shuffle_kernel(ConvK k) {
 }
 
 bool use_upsample(const dbsr_conv_desc* d, const ConvK& k) {
-    return d->x.dtype == DBSR_BF16 && d->y.dtype == DBSR_BF16 && !d->precise && d->out_mode == DBSR_OUT_SHUFFLE && !d->gate.ptr &&
+    return is16(d->x.dtype) && d->y.dtype == d->x.dtype && !d->precise && d->out_mode == DBSR_OUT_SHUFFLE && !d->gate.ptr &&
            d->kh == 1 && d->kw == 1 && d->stride == 1 && d->pad == 0 && k.cps == 32 &&
            (d->shuffle * d->shuffle) % 8 == 0 && k.Kp % 32 == 0 && k.Kp <= 128 && d->y.ld % 8 == 0 &&
            d->y.c0 % 8 == 0 && g_tiled_enabled;
 }
 
+template <typename T>
 int launch_upsample(const ConvK& k, hipStream_t s) {
     const int pg = (k.npix + 63) / 64 >= 512 ? 4 : 2;
     const unsigned grid = (unsigned)((k.npix + pg * 16 - 1) / (pg * 16));
     const int ks = k.Kp / 32;
 #define DBSR_UP(PG, KS) \
-    if (pg == PG && ks == KS) hipLaunchKernelGGL((upsample_shuffle_kernel<PG, KS>), dim3(grid), dim3(512), 0, s, k)
+    if (pg == PG && ks == KS) hipLaunchKernelGGL((upsample_shuffle_kernel<T, PG, KS>), dim3(grid), dim3(512), 0, s, k)
     DBSR_UP(2, 1); DBSR_UP(2, 2); DBSR_UP(2, 3); DBSR_UP(2, 4);
     DBSR_UP(4, 1); DBSR_UP(4, 2); DBSR_UP(4, 3); DBSR_UP(4, 4);
 #undef DBSR_UP
@@ -1306,7 +1325,7 @@ ConvK make_convk(const dbsr_conv_desc* d) {
     ConvK k;
     k.x = d->x.ptr; k.x_is = d->x.img_stride; k.x_ld = d->x.ld; k.xm = d->x.map; k.in_h = d->in_h; k.in_w = d->in_w;
     // the channel offset is folded into the base pointer (x.c0 is a multiple of 8)
-    const int esz = d->x.dtype == DBSR_BF16 ? 2 : 4;
+    const int esz = esize(d->x.dtype);
     k.x = (const char*)d->x.ptr + (long long)d->x.c0 * esz;
     const int CG = cin_pad(d->cin) / 8;
     k.CG = CG; k.KG = d->kh * d->kw * CG; k.KGp = round_up(k.KG, 4); k.Kp = k.KGp * 8;
@@ -1374,7 +1393,7 @@ extern "C" int dbsr_conv_pack_weights(const float* w_f32, const float* bias_f32,
                                       int dtype, int shuffle, void* w_packed, float* bias_out, void* stream) {
     DBSR_CHECK_ARG(w_f32 && w_packed, "pack_weights: null pointer");
     DBSR_CHECK_ARG(cout > 0 && cin > 0 && kh > 0 && kw > 0, "pack_weights: bad shape");
-    DBSR_CHECK_ARG(dtype == DBSR_F32 || dtype == DBSR_BF16, "pack_weights: bad dtype");
+    DBSR_CHECK_ARG(dtype == DBSR_F32 || is16(dtype), "pack_weights: bad dtype");
     if (shuffle > 1)
         DBSR_CHECK_ARG(cout % (shuffle * shuffle) == 0 && (cout / (shuffle * shuffle)) % 4 == 0,
                        "pack_weights: cout %d not divisible for shuffle %d", cout, shuffle);
@@ -1382,10 +1401,10 @@ extern "C" int dbsr_conv_pack_weights(const float* w_f32, const float* bias_f32,
     const int cout_pad = round_up(cout, 64);
     const long long total = (long long)cout_pad * Kp;
     hipLaunchKernelGGL(pack_weights_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                       w_f32, bias_f32, cout, cin, kh, kw, CG, KG, Kp, cout_pad, shuffle, dtype == DBSR_BF16 ? 1 : 0,
+                       w_f32, bias_f32, cout, cin, kh, kw, CG, KG, Kp, cout_pad, shuffle, dtype,
                        w_packed, bias_out);
     DBSR_LAUNCH_CHECK();
-    if (has_pipe_copy(cin, kh, kw) && dtype == DBSR_BF16) {
+    if (has_pipe_copy(cin, kh, kw) && is16(dtype)) {
         hipLaunchKernelGGL(pack_weights_pipe_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
                            (hipStream_t)stream, (const bf16_t*)w_packed, CG, Kp, cout <= 32 ? 32 : 64, total,
                            (bf16_t*)w_packed + total);
@@ -1397,7 +1416,7 @@ extern "C" int dbsr_conv_pack_weights(const float* w_f32, const float* bias_f32,
 extern "C" int dbsr_conv2d(const dbsr_conv_desc* d, void* stream) {
     DBSR_CHECK_ARG(d, "conv2d: null desc");
     DBSR_CHECK_ARG(d->x.ptr && d->w && d->y.ptr, "conv2d: null pointer");
-    DBSR_CHECK_ARG(d->x.dtype == DBSR_F32 || d->x.dtype == DBSR_BF16, "conv2d: bad input dtype");
+    DBSR_CHECK_ARG(d->x.dtype == DBSR_F32 || is16(d->x.dtype), "conv2d: bad input dtype");
     DBSR_CHECK_ARG(d->y.dtype == DBSR_F32 || d->y.dtype == d->x.dtype, "conv2d: output dtype must be f32 or input dtype");
     DBSR_CHECK_ARG(d->n_frames > 0 && d->in_h > 0 && d->in_w > 0 && d->out_h > 0 && d->out_w > 0, "conv2d: bad sizes");
     DBSR_CHECK_ARG(d->cin > 0 && d->cout > 0 && d->kh > 0 && d->kw > 0 && d->stride > 0 && d->dil > 0, "conv2d: bad shape");
@@ -1425,6 +1444,13 @@ extern "C" int dbsr_conv2d(const dbsr_conv_desc* d, void* stream) {
 
     ConvK k = make_convk(d);
     hipStream_t s = (hipStream_t)stream;
+    if (d->precise && d->x.dtype == DBSR_F16) {
+        DBSR_CHECK_ARG(d->y.dtype == DBSR_F32 && d->cout <= 16, "conv2d: precise mode needs fp32 output, cout <= 16");
+        k.ksplit = 1;
+        if (k.npix >= 512 * 256) return launch_conv<float, 1, 4, f16_t>(k, s);
+        if (k.npix >= 512 * 128) return launch_conv<float, 1, 2, f16_t>(k, s);
+        return launch_conv<float, 1, 1, f16_t>(k, s);
+    }
     if (d->precise && d->x.dtype == DBSR_BF16) {
         // bf16 activations, fp32-packed weights, fp32 MFMA: small fp32-output heads (the RGB predictor)
         DBSR_CHECK_ARG(d->y.dtype == DBSR_F32 && d->cout <= 16, "conv2d: precise mode needs fp32 output, cout <= 16");
@@ -1433,7 +1459,8 @@ extern "C" int dbsr_conv2d(const dbsr_conv_desc* d, void* stream) {
         if (k.npix >= 512 * 128) return launch_conv<float, 1, 2, bf16_t>(k, s);
         return launch_conv<float, 1, 1, bf16_t>(k, s);
     }
-    if (use_upsample(d, k)) return launch_upsample(k, s);
+    if (use_upsample(d, k)) return d->x.dtype == DBSR_F16 ? launch_upsample<f16_t>(k, s) : launch_upsample<bf16_t>(k, s);
+    if (d->x.dtype == DBSR_F16) return dispatch_conv<f16_t>(k, d, s);
     return d->x.dtype == DBSR_BF16 ? dispatch_conv<bf16_t>(k, d, s) : dispatch_conv<float>(k, d, s);
 }
 
@@ -1446,9 +1473,10 @@ extern "C" int dbsr_conv2d_head(const dbsr_conv_desc* d, const float* head_w, co
     DBSR_CHECK_ARG(head_out.dtype == DBSR_F32 && head_out.map.fpg > 0, "conv2d_head: fp32 NCHW output");
     DBSR_CHECK_ARG(d->x.ld % 8 == 0 && d->x.c0 % 8 == 0 && d->x.c0 + cin_pad(d->cin) <= d->x.ld,
                    "conv2d_head: bad input slice");
-    DBSR_CHECK_ARG(d->res.dtype == DBSR_BF16 && d->res.map.fpg > 0, "conv2d_head: residual must be bf16");
+    DBSR_CHECK_ARG(d->res.dtype == d->x.dtype && d->res.map.fpg > 0, "conv2d_head: residual dtype must equal input dtype");
     ConvK k = make_convk(d);
     k.head_w = head_w; k.head_b = head_b; k.head_cout = head_cout;
     k.y = head_out.ptr; k.y_f32 = 1; k.y_is = head_out.img_stride; k.y_ld = 1; k.y_c0 = 0; k.ym = head_out.map;
-    return launch_pipe<32, 64, 8>(k, d->n_frames, (hipStream_t)stream);
+    if (d->x.dtype == DBSR_F16) return launch_pipe<f16_t, 32, 64, 8>(k, d->n_frames, (hipStream_t)stream);
+    return launch_pipe<bf16_t, 32, 64, 8>(k, d->n_frames, (hipStream_t)stream);
 }

@@ -64,14 +64,14 @@ __global__ __launch_bounds__(256) void warp_kernel(int n, int h, int w, int grou
                 const f32x2_t w2 = {wt, wt};
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    const f32x2_t v = {__uint_as_float(q[e] << 16), __uint_as_float(q[e] & 0xffff0000u)};
+                    const f32x2_t v = {H16<T>::lo(q[e]), H16<T>::hi(q[e])};
                     acc[e] = __builtin_elementwise_fma(w2, v, acc[e]);
                 }
             }
         }
         u32x4_t o;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = pack_bf16x2(acc[e][0], acc[e][1]);
+        for (int e = 0; e < 4; ++e) o[e] = H16<T>::pack(acc[e][0], acc[e][1]);
         *(u32x4_t*)(img_ptr<T>(out, p) + (long long)rr * out.ld + g * 8) = o;
     } else {
         float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -94,7 +94,7 @@ __global__ __launch_bounds__(256) void warp_kernel(int n, int h, int w, int grou
 // pixels, issues all 4*PPW tap loads before consuming any (the per-pixel version had two dependent
 // memory round trips and only 4 KiB in flight per wave: latency-bound), and reads the flow with
 // wave-uniform (scalar) loads.
-template <int PPW>
+template <typename T, int PPW>
 __global__ __launch_bounds__(256) void warp512_bf16_kernel(int n, int h, int w, dbsr_tensor feat,
                                                            const float* __restrict__ flow, long long fis,
                                                            dbsr_tensor out) {
@@ -106,8 +106,8 @@ __global__ __launch_bounds__(256) void warp512_bf16_kernel(int n, int h, int w, 
     const unsigned total = (unsigned)n * hw;
     int tapoff[PPW][4];
     float tapw[PPW][4];
-    const bf16_t* fbase[PPW];
-    bf16_t* obase[PPW];
+    const T* fbase[PPW];
+    T* obase[PPW];
     bool live[PPW];
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
@@ -132,8 +132,8 @@ __global__ __launch_bounds__(256) void warp512_bf16_kernel(int n, int h, int w, 
             tapw[i][t] = ok ? ((t & 1) ? wx1 : wx0) * ((t >> 1) ? wy1 : wy0) : 0.f;
             tapoff[i][t] = ok ? (yy * w + xx) * feat.ld : 0;        // clamped: in-bounds address, weight 0
         }
-        fbase[i] = img_ptr<bf16_t>(feat, p) + lane * 8;
-        obase[i] = img_ptr<bf16_t>(out, p) + (long long)rr * out.ld + lane * 8;
+        fbase[i] = img_ptr<T>(feat, p) + lane * 8;
+        obase[i] = img_ptr<T>(out, p) + (long long)rr * out.ld + lane * 8;
     }
     u32x4_t v[PPW][4];
 #pragma unroll
@@ -148,13 +148,13 @@ __global__ __launch_bounds__(256) void warp512_bf16_kernel(int n, int h, int w, 
             const f32x2_t w2 = {tapw[i][t], tapw[i][t]};
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                const f32x2_t x2 = {__uint_as_float(v[i][t][e] << 16), __uint_as_float(v[i][t][e] & 0xffff0000u)};
+                const f32x2_t x2 = {H16<T>::lo(v[i][t][e]), H16<T>::hi(v[i][t][e])};
                 acc[e] = __builtin_elementwise_fma(w2, x2, acc[e]);
             }
         }
         u32x4_t o;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = pack_bf16x2(acc[e][0], acc[e][1]);
+        for (int e = 0; e < 4; ++e) o[e] = H16<T>::pack(acc[e][0], acc[e][1]);
         if (live[i]) *(u32x4_t*)obase[i] = o;
     }
 }
@@ -174,16 +174,16 @@ template <> struct Vec4<float> {
         *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
     }
 };
-template <> struct Vec4<bf16_t> {
-    static __device__ __forceinline__ void ld(const bf16_t* p, float (&v)[4]) {
+template <typename T> struct Vec4 {          // 16-bit storage (bf16 / fp16)
+    static __device__ __forceinline__ void ld(const T* p, float (&v)[4]) {
         uint2 q = *(const uint2*)p;
-        v[0] = __uint_as_float(q.x << 16); v[1] = __uint_as_float(q.x & 0xffff0000u);
-        v[2] = __uint_as_float(q.y << 16); v[3] = __uint_as_float(q.y & 0xffff0000u);
+        v[0] = H16<T>::lo(q.x); v[1] = H16<T>::hi(q.x);
+        v[2] = H16<T>::lo(q.y); v[3] = H16<T>::hi(q.y);
     }
-    static __device__ __forceinline__ void st(bf16_t* p, const float (&v)[4]) {
+    static __device__ __forceinline__ void st(T* p, const float (&v)[4]) {
         uint2 q;
-        q.x = pack_bf16x2(v[0], v[1]);
-        q.y = pack_bf16x2(v[2], v[3]);
+        q.x = H16<T>::pack(v[0], v[1]);
+        q.y = H16<T>::pack(v[2], v[3]);
         *(uint2*)p = q;
     }
 };
@@ -257,7 +257,7 @@ __global__ __launch_bounds__(256) void fuse_softmax_kernel(int B, int N, int hw,
                 if (weights.dtype == DBSR_F32)
                     Vec4<float>::st(img_ptr<float>(weights, b * N + n) + (long long)rr * weights.ld + c, wn);
                 else
-                    Vec4<bf16_t>::st(img_ptr<bf16_t>(weights, b * N + n) + (long long)rr * weights.ld + c, wn);
+                    Vec4<T>::st(img_ptr<T>(weights, b * N + n) + (long long)rr * weights.ld + c, wn);
             }
         }
     }
@@ -269,7 +269,7 @@ __global__ __launch_bounds__(256) void fuse_softmax_kernel(int B, int N, int hw,
 // twice the memory instructions).  All 2N loads are issued before the first use; the logits are
 // consumed once, so they are streamed with non-temporal loads, and the aux weights (written once,
 // never re-read by the forward) with non-temporal stores, keeping L2 for the feature rows.
-template <int NMAX>
+template <typename T, int NMAX>
 __global__ __launch_bounds__(256, 2) void fuse512_bf16_kernel(int B, int N, int hw, dbsr_tensor logits, dbsr_tensor ref,
                                                            dbsr_tensor oth, dbsr_tensor fused, dbsr_tensor weights) {
     const unsigned pix = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
@@ -281,9 +281,9 @@ __global__ __launch_bounds__(256, 2) void fuse512_bf16_kernel(int B, int N, int 
     for (int n = 0; n < NMAX; ++n) {
         if (n < N) {
             lr[n] = __builtin_nontemporal_load(
-                (const u32x4_t*)(img_ptr<bf16_t>(logits, b * N + n) + (long long)rr * logits.ld + c));
-            const bf16_t* fp = n == 0 ? img_ptr<bf16_t>(ref, b) + (long long)rr * ref.ld
-                                      : img_ptr<bf16_t>(oth, b * (N - 1) + n - 1) + (long long)rr * oth.ld;
+                (const u32x4_t*)(img_ptr<T>(logits, b * N + n) + (long long)rr * logits.ld + c));
+            const T* fp = n == 0 ? img_ptr<T>(ref, b) + (long long)rr * ref.ld
+                                 : img_ptr<T>(oth, b * (N - 1) + n - 1) + (long long)rr * oth.ld;
             fr[n] = *(const u32x4_t*)(fp + c);
         }
     }
@@ -295,8 +295,8 @@ __global__ __launch_bounds__(256, 2) void fuse512_bf16_kernel(int B, int N, int 
         if (n < N) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                m[2 * j] = fmaxf(m[2 * j], __uint_as_float(lr[n][j] << 16));
-                m[2 * j + 1] = fmaxf(m[2 * j + 1], __uint_as_float(lr[n][j] & 0xffff0000u));
+                m[2 * j] = fmaxf(m[2 * j], H16<T>::lo(lr[n][j]));
+                m[2 * j + 1] = fmaxf(m[2 * j + 1], H16<T>::hi(lr[n][j]));
             }
         }
     }
@@ -310,8 +310,8 @@ __global__ __launch_bounds__(256, 2) void fuse512_bf16_kernel(int B, int N, int 
             float en[8];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                en[2 * j] = __expf(__uint_as_float(lr[n][j] << 16) - m[2 * j]);
-                en[2 * j + 1] = __expf(__uint_as_float(lr[n][j] & 0xffff0000u) - m[2 * j + 1]);
+                en[2 * j] = __expf(H16<T>::lo(lr[n][j]) - m[2 * j]);
+                en[2 * j + 1] = __expf(H16<T>::hi(lr[n][j]) - m[2 * j + 1]);
             }
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
@@ -334,21 +334,21 @@ __global__ __launch_bounds__(256, 2) void fuse512_bf16_kernel(int B, int N, int 
             for (int j = 0; j < 8; ++j) wn[j] = e[n][j] * inv[j];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                acc[2 * j] = fmaf(__uint_as_float(fr[n][j] << 16), wn[2 * j], acc[2 * j]);
-                acc[2 * j + 1] = fmaf(__uint_as_float(fr[n][j] & 0xffff0000u), wn[2 * j + 1], acc[2 * j + 1]);
+                acc[2 * j] = fmaf(H16<T>::lo(fr[n][j]), wn[2 * j], acc[2 * j]);
+                acc[2 * j + 1] = fmaf(H16<T>::hi(fr[n][j]), wn[2 * j + 1], acc[2 * j + 1]);
             }
             if (weights.ptr) {
                 u32x4_t o;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(wn[2 * j], wn[2 * j + 1]);
-                __builtin_nontemporal_store(o, (u32x4_t*)(img_ptr<bf16_t>(weights, b * N + n) + (long long)rr * weights.ld + c));
+                for (int j = 0; j < 4; ++j) o[j] = H16<T>::pack(wn[2 * j], wn[2 * j + 1]);
+                __builtin_nontemporal_store(o, (u32x4_t*)(img_ptr<T>(weights, b * N + n) + (long long)rr * weights.ld + c));
             }
         }
     }
     u32x4_t o;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(acc[2 * j], acc[2 * j + 1]);
-    *(u32x4_t*)(img_ptr<bf16_t>(fused, b) + (long long)rr * fused.ld + c) = o;
+    for (int j = 0; j < 4; ++j) o[j] = H16<T>::pack(acc[2 * j], acc[2 * j + 1]);
+    *(u32x4_t*)(img_ptr<T>(fused, b) + (long long)rr * fused.ld + c) = o;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -527,6 +527,7 @@ bool vec_ok(const dbsr_tensor& t, int v) { return t.ld % v == 0 && t.c0 % v == 0
 template <typename F>
 int by_dtype(int dtype, F&& f) {
     if (dtype == DBSR_BF16) return f((bf16_t*)nullptr);
+    if (dtype == DBSR_F16) return f((f16_t*)nullptr);
     if (dtype == DBSR_F32) return f((float*)nullptr);
     dbsr_set_error("unsupported dtype %d", dtype);
     return DBSR_E_ARG;
@@ -544,10 +545,12 @@ extern "C" int dbsr_warp_bilinear(int n, int h, int w, int c, dbsr_tensor feat, 
     return by_dtype(feat.dtype, [&](auto* tag) {
         using T = std::remove_pointer_t<decltype(tag)>;
         if (sizeof(T) == 2 && groups == 64) {
+          if constexpr (sizeof(T) == 2) {
             // 4 pixels per wave (2: equal time, 8: occupancy-bound -- measured round 1)
             constexpr int PPW = 4;
-            hipLaunchKernelGGL((warp512_bf16_kernel<PPW>), dim3(nblocks(((long long)n * h * w + PPW - 1) / PPW, 4)),
+            hipLaunchKernelGGL((warp512_bf16_kernel<T, PPW>), dim3(nblocks(((long long)n * h * w + PPW - 1) / PPW, 4)),
                                dim3(256), 0, (hipStream_t)stream, n, h, w, feat, flow, flow_img_stride, out);
+          }
         } else if (groups % 64 == 0)
             hipLaunchKernelGGL((warp_kernel<T, true>), dim3(nblocks((long long)n * h * w * groups, 256)), dim3(256), 0,
                                (hipStream_t)stream, n, h, w, groups, feat, flow, flow_img_stride, out);
@@ -573,12 +576,12 @@ extern "C" int dbsr_fuse_softmax(int B, int N, int hw, int c, dbsr_tensor logits
     return by_dtype(ref.dtype, [&](auto* tag) {
         using T = std::remove_pointer_t<decltype(tag)>;
         const bool wp = groups % 64 == 0;
-        if constexpr (std::is_same_v<T, bf16_t>) {
+        if constexpr (sizeof(T) == 2) {
             if (c == 512 && vec_ok(logits, 8) && vec_ok(ref, 8) && vec_ok(fused, 8) &&
-                (N == 1 || vec_ok(oth, 8)) && (!weights.ptr || (weights.dtype == DBSR_BF16 && vec_ok(weights, 8)))) {
+                (N == 1 || vec_ok(oth, 8)) && (!weights.ptr || (weights.dtype == ref.dtype && vec_ok(weights, 8)))) {
                 const long long waves = (long long)B * hw;
 #define DBSR_FUSE512(NM)                                                                                       \
-    hipLaunchKernelGGL((fuse512_bf16_kernel<NM>), dim3(nblocks(waves, 4)), dim3(256), 0, (hipStream_t)stream, B, \
+    hipLaunchKernelGGL((fuse512_bf16_kernel<T, NM>), dim3(nblocks(waves, 4)), dim3(256), 0, (hipStream_t)stream, B, \
                        N, hw, logits, ref, oth, fused, weights);
                 if (N <= 4) {
                     DBSR_FUSE512(4)

@@ -290,6 +290,7 @@ inline unsigned nblocks(long long total, int bs) { return (unsigned)((total + bs
 template <typename F>
 int by_dtype(int dtype, F&& f) {
     if (dtype == DBSR_BF16) return f((bf16_t*)nullptr);
+    if (dtype == DBSR_F16) return f((f16_t*)nullptr);
     if (dtype == DBSR_F32) return f((float*)nullptr);
     dbsr_set_error("unsupported dtype %d", dtype);
     return DBSR_E_ARG;

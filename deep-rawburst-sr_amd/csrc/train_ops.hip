@@ -7,6 +7,7 @@
 #include "common.hpp"
 
 #include <algorithm>
+#include <type_traits>
 
 using namespace dbsr;
 
@@ -19,6 +20,7 @@ bool vec_ok(const dbsr_tensor& t, int v) { return t.ld % v == 0 && t.c0 % v == 0
 template <typename F>
 int by_dtype(int dtype, F&& f) {
     if (dtype == DBSR_BF16) return f((bf16_t*)nullptr);
+    if (dtype == DBSR_F16) return f((f16_t*)nullptr);
     if (dtype == DBSR_F32) return f((float*)nullptr);
     dbsr_set_error("unsupported dtype %d", dtype);
     return DBSR_E_ARG;
@@ -44,13 +46,20 @@ constexpr int WG_HH = WG_TH + 2, WG_HW = WG_TW + 2, WG_HPX = WG_HH * WG_HW;   //
 
 template <typename T> struct WgCfg;
 template <> struct WgCfg<bf16_t> { static constexpr int ROWB = 144; };      // 128 B + 16 B skew per pixel row
+template <> struct WgCfg<f16_t> { static constexpr int ROWB = 144; };
 template <> struct WgCfg<float> { static constexpr int ROWB = 272; };       // 256 B + 16 B
 
 typedef short v4s_t __attribute__((ext_vector_type(4)));
 struct FragB { bf16x8_t v; };
-__device__ __forceinline__ f32x4_t mma_bf16(const FragB& a, const FragB& b, f32x4_t c) {
-    typedef __attribute__((ext_vector_type(8))) __bf16 bfv;
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bfv, a.v), __builtin_bit_cast(bfv, b.v), c, 0, 0, 0);
+template <typename T>
+__device__ __forceinline__ f32x4_t mma16(const FragB& a, const FragB& b, f32x4_t c) {
+    if constexpr (std::is_same_v<T, f16_t>) {
+        typedef __attribute__((ext_vector_type(8))) _Float16 hv;
+        return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(hv, a.v), __builtin_bit_cast(hv, b.v), c, 0, 0, 0);
+    } else {
+        typedef __attribute__((ext_vector_type(8))) __bf16 bfv;
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bfv, a.v), __builtin_bit_cast(bfv, b.v), c, 0, 0, 0);
+    }
 }
 
 __device__ __forceinline__ v4s_t tr16(const unsigned char* lds_byte) {
@@ -132,7 +141,7 @@ __global__ __launch_bounds__(K == 3 ? 576 : 256) void conv_wgrad_kernel(
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) acc[i][j] = mma_bf16(a[i], b[j], acc[i][j]);
+                    for (int j = 0; j < 4; ++j) acc[i][j] = mma16<T>(a[i], b[j], acc[i][j]);
             } else {
                 // fp32: 8 MFMAs of k = 4 pixels; lane (kq = lane>>4, m = lane&15)
                 const int kq = lane >> 4, m = lane & 15;
@@ -482,7 +491,7 @@ extern "C" int dbsr_conv_wgrad(int n_frames, int h, int w, dbsr_tensor x, int ci
     DBSR_CHECK_ARG(x.dtype == dy.dtype, "conv_wgrad: x and dy dtypes differ");
     DBSR_CHECK_ARG(k == 1 || k == 3, "conv_wgrad: k must be 1 or 3 (stride 1, pad k/2)");
     DBSR_CHECK_ARG(n_frames > 0 && h > 0 && w > 0 && cin > 0 && cout > 0, "conv_wgrad: bad sizes");
-    const int esz = x.dtype == DBSR_BF16 ? 2 : 4, epp = 16 / esz;
+    const int esz = x.dtype == DBSR_F32 ? 4 : 2, epp = 16 / esz;
     DBSR_CHECK_ARG(vec_ok(x, epp) && vec_ok(dy, epp) && x.ld >= x.c0 + (cin + epp - 1) / epp * epp &&
                    dy.ld >= dy.c0 + (cout + epp - 1) / epp * epp,
                    "conv_wgrad: ld/c0 must be multiples of %d and cover the channels", epp);

@@ -79,7 +79,8 @@ class DBSRNet(nn.Module):
     """Deep Burst Super-Resolution model (models/dbsr/dbsrnet.py:24-38).
 
     Extra knobs (not in the reference; defaults keep reference behaviour):
-      compute_dtype      torch.float32 (default, parity mode) or torch.bfloat16 (throughput mode);
+      compute_dtype      torch.float32 (default, parity mode), torch.bfloat16 (throughput mode) or
+                         torch.float16 (configs[4]);
                          accumulation is fp32 in both, flows/offsets stay fp32.
       return_fusion_weights  True: aux['fusion_weights'] is produced exactly as the reference
                          returns it (shape [B,N,C,H,W]; backed by the engine's channels-last buffer).
@@ -103,8 +104,8 @@ class DBSRNet(nn.Module):
         self._engine = None
 
     def set_compute_dtype(self, dtype):
-        if dtype not in (torch.float32, torch.bfloat16):
-            raise ValueError('compute_dtype must be torch.float32 or torch.bfloat16')
+        if dtype not in (torch.float32, torch.bfloat16, torch.float16):
+            raise ValueError('compute_dtype must be torch.float32, torch.bfloat16 or torch.float16')
         self.compute_dtype = dtype
         self._engine = None
         return self

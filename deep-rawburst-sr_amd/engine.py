@@ -508,7 +508,7 @@ class DBSREngine:
         plan.max_blocks = 0
         # ---------------- warp (encoders.py:80) ----------------
         Wf = NHWC(max(P, 1), H, W, C, dt, dev)
-        es = 2 if dt == torch.bfloat16 else 4
+        es = 4 if dt == torch.float32 else 2
         if P > 0:
             plan.add('warp', lib.dbsr_warp_bilinear, P, H, W, C, E.d(0, (N - 1, N, 1, 1)), bufs['offsets'].data_ptr(),
                      2 * H * W, Wf.d(0), work=('byte', 2.0 * P * C * H * W * es + 8.0 * P * H * W))
@@ -572,7 +572,7 @@ class DBSREngine:
         # bf16: the last post ResBlock's conv2 and the RGB predictor in one kernel (its 32-channel output
         # never reaches HBM; the head runs fp32 on the fp32 ResBlock output, decoders.py:59-61)
         head = None
-        if dt == torch.bfloat16 and self.dec_post and DBSREngine.FUSED_HEAD:
+        if dt != torch.float32 and self.dec_post and DBSREngine.FUSED_HEAD:
             head = ('predictor', self.head_w, self.head_b, pdesc)
         if head is not None:
             i, fused = self._resblocks(plan, 'dec.post', self.dec_post, B, (H * S, W * S), sh, a, dt, head=head)
@@ -580,7 +580,7 @@ class DBSREngine:
             i, fused = self._resblocks(plan, 'dec.post', self.dec_post, B, (H * S, W * S), sh, a, dt), False
         if not fused:
             plan.conv('dec.predictor', self.pred, B, sh[i], 0, (H * S, W * S), None, 0, L.ACT_RELU,
-                      out_mode=L.OUT_NCHW_F32, y_desc=pdesc, precise=(dt == torch.bfloat16))
+                      out_mode=L.OUT_NCHW_F32, y_desc=pdesc, precise=(dt != torch.float32))
         plan.keep.extend([g, sh])
 
     @staticmethod

@@ -40,7 +40,7 @@ extern "C" {
 
 #define DBSR_ABI_VERSION 7
 
-enum { DBSR_F32 = 0, DBSR_BF16 = 1 };
+enum { DBSR_F32 = 0, DBSR_BF16 = 1, DBSR_F16 = 2 };
 enum { DBSR_ACT_NONE = 0, DBSR_ACT_RELU = 1, DBSR_ACT_LRELU = 2 };      /* LeakyReLU slope 0.1 */
 enum { DBSR_OUT_NHWC = 0, DBSR_OUT_SHUFFLE = 1, DBSR_OUT_NCHW_F32 = 2 };
 enum { DBSR_E_ARG = -1, DBSR_E_UNSUPPORTED = -2 };
@@ -57,7 +57,7 @@ typedef struct dbsr_frame_map {
 
 typedef struct dbsr_tensor {          /* a channel slice of a batch of NHWC images */
     void* ptr;
-    int dtype;                        /* DBSR_F32 / DBSR_BF16 */
+    int dtype;                        /* DBSR_F32 / DBSR_BF16 / DBSR_F16 */
     long long img_stride;             /* elements between stored images */
     int ld;                           /* elements between pixels */
     int c0;                           /* first channel */

@@ -167,3 +167,65 @@ def test_pipe_epilogue_variants(ops_mod, case):
 def ops_mod():
     from dbsr_amd import ops as O
     return O
+
+
+@pytest.fixture(scope='module')
+def cfg4_case():
+    """configs[4]: SyntheticBurst 14 frames 96x96 -> x8 of full resolution (upsample_factor 16, 1536x1536
+    output; SURVEY §8d's reading of '8x'), seeded weights of that architecture, and the oracle's fp32
+    forward."""
+    import dbsr_amd
+    from dbsr_amd import arch
+    from dbsr_amd.weights import generate_state_dict
+    from dbsr_amd.burst import synthetic_bursts
+    from oracle import dbsr_oracle as orc
+    kw = dict(dbsr_amd.DBSR_SYNTHETIC_KWARGS, upsample_factor=16)
+    net = dbsr_amd.dbsrnet_cvpr2021(**kw)
+    sd = {k: torch.from_numpy(v) for k, v in generate_state_dict(arch.state_dict_shapes(net), seed=0).items()}
+    net.load_state_dict(sd)
+    burst, gt = synthetic_bursts(1, 14, 96, 96, sr_factor=16, seed=31)
+    okw = dict(orc.DBSR_SYNTHETIC_KWARGS, upsample_factor=16)
+    with torch.no_grad():
+        ref, raux = orc.dbsr_forward(burst, sd, kw=okw)
+    return net, burst, gt, ref, raux['offsets']
+
+
+def _psnr_delta(pred, ref, gt):
+    return max(abs(a - b) for a, b in zip(_psnr_q(pred.float().cpu(), gt), _psnr_q(ref, gt)))
+
+
+def test_cfg5_fp16_x16_unsharded(cfg4_case):
+    """configs[4]'s network (x16, 96x96, fp16 compute on the f16 MFMA kernels) in one piece vs the oracle."""
+    net, burst, gt, ref, roffs = cfg4_case
+    net = net.to(DEV).set_compute_dtype(torch.float16)
+    with torch.no_grad():
+        pred, aux = net(burst.to(DEV))
+    assert pred.shape == (1, 3, 1536, 1536)
+    od = (aux['offsets'].cpu() - roffs).abs().max().item()
+    dp = _psnr_delta(pred, ref, gt)
+    print('fp16 x16: offsets max-abs %.4g PSNR delta %.5f dB pred max-abs %.4g' % (
+        od, dp, (pred.float().cpu() - ref).abs().max().item()))
+    assert od <= OFFS_TOL
+    assert dp <= 0.01
+
+
+def test_cfg5_frame_sharded_4_ranks_fp16(cfg4_case):
+    """configs[4] as specified: frames split over 4 ranks (simulated on one device: each rank's
+    forward_partial on its frame shard, statistics stacked as the RCCL all-gather lays them out), fp16,
+    x16 upsampling, 96x96 -> combine_decode equals the unsharded oracle forward within the bar."""
+    from dbsr_amd.parallel import frame_shard
+    net, burst, gt, ref, _ = cfg4_case
+    net = net.to(DEV).set_compute_dtype(torch.float16)
+    eng = net._get_engine()
+    b = burst.to(DEV)
+    with torch.no_grad():
+        stats = []
+        for r in range(4):
+            frames, first = frame_shard(14, r, 4)
+            st, _ = eng.forward_partial(b[:, frames], first)
+            stats.append(st.clone())
+        pred = eng.combine_decode(torch.stack(stats))
+    dp = _psnr_delta(pred, ref, gt)
+    print('fp16 x16 4-rank frame-sharded: PSNR delta %.5f dB' % dp)
+    assert pred.shape == (1, 3, 1536, 1536)
+    assert dp <= 0.01
