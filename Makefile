@@ -10,7 +10,14 @@ CPPSRCS := $(wildcard $(SRC)/*.cpp)
 OBJS    := $(patsubst $(SRC)/%.hip,$(OBJDIR)/%.o,$(HIPSRCS)) $(patsubst $(SRC)/%.cpp,$(OBJDIR)/%.o,$(CPPSRCS))
 FLAGS   := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Iinclude -Wall -Wno-unused-function
 
-all: $(LIB)
+# torch.ops.dbsr.* operator library (TORCH_LIBRARY over the C ABI; loaded by dbsr_amd/torch_ops.py)
+TORCH_DIR := $(shell python3 -c "import torch, os; print(os.path.dirname(torch.__file__))")
+TORCH_LIB := $(PKG)/libdbsr_torch.so
+TORCH_FLAGS := --offload-arch=$(ARCH) -O2 -std=c++17 -fPIC -D_GLIBCXX_USE_CXX11_ABI=1 -DUSE_ROCM=1 \
+	-I$(TORCH_DIR)/include -I$(TORCH_DIR)/include/torch/csrc/api/include -Iinclude -Wno-unused-result \
+	-Wno-deprecated-declarations
+
+all: $(LIB) $(TORCH_LIB)
 
 $(OBJDIR)/%.o: $(SRC)/%.hip $(SRC)/common.hpp include/dbsr_hip.h
 	@mkdir -p $(OBJDIR)
@@ -34,6 +41,12 @@ exp:
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(EXP_LIB) $(OBJDIR)/$(EXP_NAME)/*.o
 
 clean:
-	rm -rf $(OBJDIR) $(LIB) $(PKG)/libdbsr_hip_*.so
+	rm -rf $(OBJDIR) $(LIB) $(TORCH_LIB) $(PKG)/libdbsr_hip_*.so
 
 .PHONY: all clean exp
+
+torchops: $(TORCH_LIB)
+$(TORCH_LIB): $(SRC)/torch/torch_ops.cpp include/dbsr_hip.h $(LIB)
+	$(HIPCC) $(TORCH_FLAGS) -shared -o $@ $(SRC)/torch/torch_ops.cpp -L$(TORCH_DIR)/lib -lc10 -lc10_hip -ltorch \
+		-ltorch_cpu -ltorch_hip -L$(PKG) -ldbsr_hip -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(TORCH_DIR)/lib
+.PHONY: torchops

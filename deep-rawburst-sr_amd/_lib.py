@@ -73,6 +73,8 @@ def lib():
             'dbsr_conv2d_head': ([ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_int, Tensor, c_void_p], c_int),
             'dbsr_conv_head_ok': ([ctypes.POINTER(ConvDesc)], c_int),
             'dbsr_correlation': ([c_int, c_int, c_int, c_int, Tensor, Tensor, Tensor, c_int, c_void_p], c_int),
+            'dbsr_correlation_backward': ([c_int, c_int, c_int, c_int, Tensor, Tensor, Tensor, Tensor, c_int, Tensor,
+                                           Tensor, c_void_p], c_int),
             'dbsr_backwarp': ([c_int, c_int, c_int, c_int, Tensor, Tensor, c_float, Tensor, c_void_p], c_int),
             'dbsr_warp_bilinear': ([c_int, c_int, c_int, c_int, Tensor, c_void_p, c_ll, Tensor, c_void_p], c_int),
             'dbsr_fuse_softmax': ([c_int, c_int, c_int, c_int, Tensor, Tensor, Tensor, Tensor, Tensor, c_void_p],
@@ -119,7 +121,7 @@ def lib():
 EXPORTED = ['dbsr_abi_version', 'dbsr_last_error', 'dbsr_conv_packed_elems', 'dbsr_conv_pack_weights', 'dbsr_conv2d',
             'dbsr_set_conv_algo', 'dbsr_conv_kernel_for', 'dbsr_conv_workspace_bytes', 'dbsr_conv2d_head',
             'dbsr_conv_head_ok',
-            'dbsr_correlation', 'dbsr_backwarp', 'dbsr_warp_bilinear', 'dbsr_fuse_softmax',
+            'dbsr_correlation', 'dbsr_correlation_backward', 'dbsr_backwarp', 'dbsr_warp_bilinear', 'dbsr_fuse_softmax',
             'dbsr_fuse_partial', 'dbsr_fuse_combine',
             'dbsr_conv_transpose_k4s2', 'dbsr_pack_burst', 'dbsr_flow_finalize', 'dbsr_gauss_blur3',
             'dbsr_merge_prep', 'dbsr_pwc_assemble', 'dbsr_zero', 'dbsr_conv_wgrad_workspace_bytes', 'dbsr_conv_wgrad',

@@ -45,6 +45,56 @@ __global__ void correlation_kernel(int n, int h, int w, int C, dbsr_tensor f1, d
     elem<T>::st(img_ptr<T>(out, p) + (long long)rr * out.ld + d, v);
 }
 
+// Cost-volume backward (correlation.py:105-233, K3/K4: updateGradFirst / updateGradSecond), with the
+// callers' LeakyReLU(0.1) folded in when leaky != 0 (slope from the sign of the forward output):
+//   g[d](y,x)     = gout[d](y,x) * (leaky && out[d](y,x) <= 0 ? 0.1 : 1)
+//   dfirst(y,x)   = 1/C sum_d g[d](y,x) * second(y+dy, x+dx)
+//   dsecond(y,x)  = 1/C sum_d g[d](y-dy,x-dx) * first(y-dy, x-dx)
+// both as gathers (no atomics): one thread per (pair, pixel, 8-channel group).
+template <typename T>
+__global__ void correlation_bwd_kernel(int n, int h, int w, int C, dbsr_tensor f1, dbsr_tensor f2, dbsr_tensor out,
+                                       dbsr_tensor gout, int leaky, dbsr_tensor d1, dbsr_tensor d2) {
+    const int groups = (C + 7) / 8;
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long long)n * h * w * groups) return;
+    const int g = (int)(idx % groups);
+    const long long pix = idx / groups;
+    const int p = (int)(pix / (h * w)), rr = (int)(pix - (long long)p * h * w);
+    const int y = rr / w, x = rr - y * w;
+    const int c0 = g * 8, nc = min(8, C - c0);
+    float a1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, a2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    auto grad_at = [&](int yy, int xx, int d) {
+        const long long o = (long long)(yy * w + xx);
+        float gv = elem<T>::ld(img_ptr<T>(gout, p) + o * gout.ld + d);
+        if (leaky && elem<T>::ld(img_ptr<T>(out, p) + o * out.ld + d) <= 0.f) gv *= 0.1f;
+        return gv;
+    };
+    for (int d = 0; d < 81; ++d) {
+        const int dy = d / 9 - 4, dx = d % 9 - 4;
+        // dfirst: second at (y+dy, x+dx)
+        const int y2 = y + dy, x2 = x + dx;
+        if ((unsigned)y2 < (unsigned)h && (unsigned)x2 < (unsigned)w) {
+            const float gv = grad_at(y, x, d);
+            const T* b = img_ptr<T>(f2, p) + ((long long)y2 * w + x2) * f2.ld + c0;
+            for (int j = 0; j < nc; ++j) a1[j] = fmaf(gv, elem<T>::ld(b + j), a1[j]);
+        }
+        // dsecond: output pixel (y-dy, x-dx) used this pixel of `second` at displacement d
+        const int y1 = y - dy, x1 = x - dx;
+        if ((unsigned)y1 < (unsigned)h && (unsigned)x1 < (unsigned)w) {
+            const float gv = grad_at(y1, x1, d);
+            const T* a = img_ptr<T>(f1, p) + ((long long)y1 * w + x1) * f1.ld + c0;
+            for (int j = 0; j < nc; ++j) a2[j] = fmaf(gv, elem<T>::ld(a + j), a2[j]);
+        }
+    }
+    const float inv = 1.0f / (float)C;
+    T* o1 = img_ptr<T>(d1, p) + (long long)rr * d1.ld + c0;
+    T* o2 = img_ptr<T>(d2, p) + (long long)rr * d2.ld + c0;
+    for (int j = 0; j < nc; ++j) {
+        elem<T>::st(o1 + j, a1[j] * inv);
+        elem<T>::st(o2 + j, a2[j] * inv);
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 // backwarp (pwcnet.py:16-38): grid = linspace(-1+1/W, 1-1/W) + flow/((W-1)/2), grid_sample bilinear
 // zeros align_corners=False, then mask = (sampled ones-channel > 0.999).  The ones-channel is the
@@ -311,6 +361,24 @@ extern "C" int dbsr_correlation(int n, int h, int w, int c, dbsr_tensor first, d
         using T = std::remove_pointer_t<decltype(tag)>;
         hipLaunchKernelGGL(correlation_kernel<T>, dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, n, h,
                            w, c, first, second, out, leaky, vec);
+        DBSR_LAUNCH_CHECK();
+        return 0;
+    });
+}
+
+extern "C" int dbsr_correlation_backward(int n, int h, int w, int c, dbsr_tensor first, dbsr_tensor second,
+                                         dbsr_tensor out, dbsr_tensor gout, int leaky, dbsr_tensor dfirst,
+                                         dbsr_tensor dsecond, void* stream) {
+    DBSR_CHECK_ARG(map_ok(first) && map_ok(second) && map_ok(gout) && map_ok(dfirst) && map_ok(dsecond) &&
+                   (!leaky || map_ok(out)), "correlation_backward: bad tensor");
+    DBSR_CHECK_ARG(first.dtype == second.dtype && gout.dtype == first.dtype && dfirst.dtype == first.dtype &&
+                   dsecond.dtype == first.dtype && (!leaky || out.dtype == first.dtype), "correlation_backward: dtype");
+    DBSR_CHECK_ARG(n > 0 && h > 0 && w > 0 && c > 0 && gout.c0 + 81 <= gout.ld, "correlation_backward: sizes");
+    const long long total = (long long)n * h * w * ((c + 7) / 8);
+    return by_dtype(first.dtype, [&](auto* tag) {
+        using T = std::remove_pointer_t<decltype(tag)>;
+        hipLaunchKernelGGL(correlation_bwd_kernel<T>, dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, n,
+                           h, w, c, first, second, out, gout, leaky, dfirst, dsecond);
         DBSR_LAUNCH_CHECK();
         return 0;
     });

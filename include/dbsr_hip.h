@@ -132,6 +132,12 @@ size_t dbsr_conv_workspace_bytes(const dbsr_conv_desc* d);
 int dbsr_correlation(int n_pairs, int h, int w, int c, dbsr_tensor first, dbsr_tensor second,
                      dbsr_tensor out, int leaky, void* stream);
 
+/* Backward of dbsr_correlation (correlation.py:105-233, K3/K4) w.r.t. both inputs: gout = dL/d(out),
+ * out = the forward output (read only when leaky != 0, for the LeakyReLU slope). */
+int dbsr_correlation_backward(int n_pairs, int h, int w, int c, dbsr_tensor first, dbsr_tensor second,
+                              dbsr_tensor out, dbsr_tensor gout, int leaky, dbsr_tensor dfirst, dbsr_tensor dsecond,
+                              void* stream);
+
 /* PWC-Net backwarp of `in` (C channels) by flow*scale (flow: NHWC fp32 slice with 2 channels),
  * bilinear, zero padding, validity mask (weight mass > 0.999). */
 int dbsr_backwarp(int n, int h, int w, int c, dbsr_tensor in, dbsr_tensor flow, float scale,

@@ -108,3 +108,18 @@ def test_product_refuses_cpu_tensors():
         net(torch.zeros(1, 3, 4, 48, 48))
     with pytest.raises(NotImplementedError):
         ops.FunctionCorrelation(torch.zeros(1, 8, 4, 4), torch.zeros(1, 8, 4, 4))
+
+
+def test_torch_ops_registered():
+    """libdbsr_torch.so registers the TORCH_LIBRARY(dbsr) schemas with autograd formulas."""
+    import torch
+    from dbsr_amd import torch_ops
+    torch_ops.load()
+    names = ['correlation', 'correlation_backward', 'backwarp', 'warp_bilinear', 'warp_bilinear_backward',
+             'fuse_softmax', 'fuse_backward', 'conv2d_fused']
+    for n in names:
+        assert hasattr(torch.ops.dbsr, n), n
+    assert 'bool leaky=False' in str(torch.ops.dbsr.correlation.default._schema)
+    # HIP implementations only (no CPU kernel, like correlation.py:324-325): CPU tensors fail loudly
+    with pytest.raises(NotImplementedError, match="dbsr::correlation.*CPU"):
+        torch.ops.dbsr.correlation(torch.zeros(1, 4, 3, 3), torch.zeros(1, 4, 3, 3))
