@@ -14,10 +14,10 @@ import statistics
 import sys
 
 KERNELS = {   # label -> (name predicate, algorithmic bytes per launch at the default bench workload)
-    'warp kernel (DBSR warp, encoders.py:80; warp_proj_kernel: + merging.py:76-78 projection)':
-        (lambda n: ('warp_kernel' in n and 'backwarp' not in n) or 'warp512_bf16_kernel' in n or 'warp_proj_kernel' in n, None),
+    'warp kernel (DBSR warp, encoders.py:80)':
+        (lambda n: ('warp_kernel' in n and 'backwarp' not in n and '_bwd' not in n) or 'warp512_bf16_kernel' in n, None),
     'fusion kernel (merging.py:116-126)': (lambda n: 'fuse_softmax_kernel' in n or 'fuse512_bf16_kernel' in n, None),
-    'conv3x3_pipe_kernel, largest grid (wp.out 128->512)': (lambda n: 'conv3x3_pipe_kernel<64, 48, 8, 3>' in n, None),
+    'conv3x3_pipe_kernel, largest grid (wp.out 128->512)': (lambda n: 'conv3x3_pipe_kernel<' in n and '64, 48, 8, 3>' in n, None),
 }
 
 
