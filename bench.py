@@ -176,7 +176,8 @@ def main():
     dom = max((k for k in fam if k.startswith('conv')), key=lambda k: fam[k][0])
     t_ms, t_flop, t_n = fam[dom]
     t_tf = t_flop / (t_ms * 1e-3) / 1e12
-    kdesc = {'conv3x3_pipe': 'conv3x3_pipe_kernel (persistent LDS-DMA-pipelined implicit-GEMM 3x3',
+    kdesc = {'conv3x3_ws': 'conv3x3_ws_kernel (persistent weight-stationary implicit-GEMM 3x3, Cin <= 64',
+             'conv3x3_pipe': 'conv3x3_pipe_kernel (persistent LDS-DMA-pipelined implicit-GEMM 3x3',
              'conv3x3_tiled': 'conv3x3_tiled_kernel (LDS-tiled implicit-GEMM 3x3',
              'conv2d_generic': 'conv2d_kernel (generic implicit-GEMM'}[dom]
     roof = {'bound': 'mfma', 'kernel': kdesc + ', %d launches per forward; '

@@ -424,6 +424,17 @@ __device__ __forceinline__ void glds16(const void* src, u32x4_t* lds_piece) {
     __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_piece, 16, 0, 0);
 }
 
+// Buffer-resource LDS-DMA (buffer_load_dwordx4 ... lds): a lane whose byte offset lies past the
+// resource's num_records gets zeros written to LDS, so halo pixels outside the frame need neither a
+// zero page nor a per-lane pointer select; soffset carries the wave-uniform part of the address.
+constexpr int BUF_OOB = (int)0x80000000u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, unsigned bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t r, int voff, int soff, u32x4_t* lds_piece) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_piece, 16, voff, soff, 0, 0);
+}
+
 template <typename T, int WM, int WN, int D>
 __global__ __launch_bounds__(256, 2) void conv3x3_tiled_kernel(ConvK k, int tiles_x, int tiles_y, int nct,
                                                                int nblocks) {
@@ -757,6 +768,22 @@ struct PipeCfg {
 // each of its four 16-lane groups, the 4 lanes with equal p mod 4 read 4 distinct phys values.
 __device__ __forceinline__ int halo_phys(int p, int g) { return 2 * (g & 1) + ((g >> 1) ^ ((p >> 2) & 1)); }
 
+// Diagnostic build only (make exp EXP_FLAGS=-DDBSR_PIPE_STAMPS): per-wave s_memtime stamps around each
+// stage's barrier and tap loop, read back by dbsr_diag_pipe_stamps (tools/pipe_stamps.py).  The product
+// build compiles none of this.
+#ifdef DBSR_PIPE_STAMPS
+constexpr int STAMP_STAGES = 24, STAMP_EV = 5;
+__device__ unsigned long long g_pipe_stamps[256 * 8 * (STAMP_STAGES * STAMP_EV + 2)];
+#define PIPE_STAMP(slot)                                                                                        \
+    do {                                                                                                       \
+        const int sl_ = (slot);                                                                                \
+        if (lane == 0 && blockIdx.x < 256 && sl_ < STAMP_STAGES * STAMP_EV + 2)                                 \
+            g_pipe_stamps[(blockIdx.x * 8 + wave) * (STAMP_STAGES * STAMP_EV + 2) + sl_] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define PIPE_STAMP(slot) do { } while (0)
+#endif
+
 template <typename T, int WM, int TW, int TH, int EPI>
 __global__ __launch_bounds__(512, 1) void conv3x3_pipe_kernel(ConvK k, int tiles_x, int tiles_y, int nct,
                                                               int ntiles) {
@@ -765,7 +792,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pipe_kernel(ConvK k, int tiles
     __shared__ __attribute__((aligned(16))) u32x4_t lds[C::LDS_U4];
     float* lbias = (float*)(lds + 2 * C::STAGE_U4);      // [nct * WM] fp32
 
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // uniform: scalar DMA offsets
     const int g = lane >> 4, col = lane & 15;
     const int nchunks = k.CG / 4;
     // epilogue variants (compile-time where the forward's convs need them): 1 act(ReLU), 2 conv + residual
@@ -801,6 +828,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pipe_kernel(ConvK k, int tiles
     const int pb = (b & 7) * (grid >> 3) + (b >> 3);
     const int my_tiles = pb < ntiles ? (ntiles - pb + grid - 1) / grid : 0;
     if (my_tiles == 0) return;
+    PIPE_STAMP(0);
 
     // tile descriptors hold wave-uniform values only (scalar registers); the lane's own pixel/cout offset
     // within a tile is the same for every tile
@@ -826,27 +854,38 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pipe_kernel(ConvK k, int tiles
 
     // one 1-KiB DMA piece of stage (tile t, chunk c): piece `it` of this wave is item wave + 8*it of the
     // stage image (clamped: surplus slots re-issue the last piece, an identical write, so every wave
-    // issues exactly PER pieces); addresses are computed at issue time, between MFMAs
+    // issues exactly PER pieces).  Halo pieces: the lane's (halo row, column, k-group) and its byte
+    // offset from the halo origin are tile-invariant and precomputed; per piece only the frame bounds
+    // test and one add remain (out-of-frame lanes read past the buffer resource and land zeros).
+    // Weight pieces are contiguous 1 KiB: a uniform soffset on a constant lane offset.
+    constexpr int HPER = (C::IN_ITEMS + C::NWAVES - 1) / C::NWAVES;   // halo pieces per wave (upper bound)
+    int h_rc[HPER], h_off[HPER];
+    const int pix_b = k.x_ld * (int)sizeof(T);
+#pragma unroll
+    for (int it = 0; it < HPER; ++it) {
+        const int p = (wave + C::NWAVES * it) * 16 + (lane >> 2), ph = lane & 3;
+        const int gg = 2 * ((ph & 1) ^ ((p >> 2) & 1)) + (ph >> 1);
+        const int r = p / C::HWD, cc = p - r * C::HWD;
+        h_rc[it] = p < C::NQ ? (r << 16) | cc : 0x7fff7fff;    // rows/cols past the halo never pass the test
+        h_off[it] = (r * k.in_w + cc) * pix_b + gg * 16;
+    }
+    const __amdgpu_buffer_rsrc_t w_rsrc = buf_rsrc(k.w_pipe, 0xffffffffu);
+    const unsigned frame_bytes = (unsigned)((long long)k.in_h * k.in_w * pix_b);
     auto dma = [&](int it, const Tile& t, int c, int buf) {
         const int item = min(wave + C::NWAVES * it, C::ITEMS - 1);
-        const char* src;
-        if (item < C::IN_ITEMS) {
-            // lane -> (halo pixel, physical k-group slot) -> logical k-group (inverse of halo_phys)
-            const int p = item * 16 + (lane >> 2), ph = lane & 3;
-            const int gg = 2 * ((ph & 1) ^ ((p >> 2) & 1)) + (ph >> 1);
-            const int r = p / C::HWD, cc = p - (p / C::HWD) * C::HWD;
-            const int iy = t.y0 - 1 + r, ix = t.x0 - 1 + cc;
-            src = (p < C::NQ && (unsigned)iy < (unsigned)k.in_h && (unsigned)ix < (unsigned)k.in_w)
-                      ? (const char*)(t.xf + ((long long)iy * k.in_w + ix) * k.x_ld + c * 32 + gg * 8)
-                      : (const char*)g_dbsr_zero16;
+        u32x4_t* dst = lds + buf * C::STAGE_U4 + item * 64;
+        if (it < HPER && item < C::IN_ITEMS) {
+            const int hy = t.y0 - 1 + (h_rc[it] >> 16), hx = t.x0 - 1 + (h_rc[it] & 0xffff);
+            const bool ok = (unsigned)hy < (unsigned)k.in_h && (unsigned)hx < (unsigned)k.in_w;
+            const int base = ((t.y0 - 1) * k.in_w + (t.x0 - 1)) * pix_b + c * 64;
+            blds16(buf_rsrc(t.xf, frame_bytes), ok ? base + h_off[it] : BUF_OOB, 0, dst);
         } else {
             // chunk-major weight copy: one contiguous 1-KiB piece per (16-cout block, chunk, tap)
             const int wi = item - C::IN_ITEMS;
             const int tap = wi / (WM / 16), blk = wi % (WM / 16);
-            const long long piece = ((long long)((t.cb >> 4) + blk) * nchunks + c) * 9 + tap;
-            src = (const char*)((const T*)k.w_pipe + piece * 512 + lane * 8);
+            const int piece = (((t.cb >> 4) + blk) * nchunks + c) * 9 + tap;
+            blds16(w_rsrc, lane * 16, piece * 1024, dst);
         }
-        glds16(src, lds + buf * C::STAGE_U4 + item * 64);
     };
 
     f32x4_t acc[WM / 16][C::GW];
@@ -941,7 +980,13 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pipe_kernel(ConvK k, int tiles
     // residual loads (last stage) and the next stage's DMA pieces (taps 0-5).
     for (int ti = 0; ti < my_tiles; ++ti) {
         for (int c = 0; c < nchunks; ++c, ++s) {
+            PIPE_STAMP(2 + s * 5);
+#ifdef DBSR_PIPE_STAMPS
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            PIPE_STAMP(3 + s * 5);
+#endif
             __syncthreads();            // stage s landed (vmcnt(0) + barrier); stage s-1 fully consumed
+            PIPE_STAMP(4 + s * 5);
             const bool fin = c == 0 && ti > 0;
             if (fin) epilogue(prev);
             const bool last = c == nchunks - 1;
@@ -990,6 +1035,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pipe_kernel(ConvK k, int tiles
             read_frags(0, a0, b0);
 #pragma unroll
             for (int tap = 0; tap < 9; tap += 2) {
+                if (tap == 6) PIPE_STAMP(5 + s * 5);
                 vmem(tap);
                 if (tap + 1 < 9) read_frags(tap + 1, a1, b1);
                 mfmas(a0, b0);
@@ -999,6 +1045,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pipe_kernel(ConvK k, int tiles
                     mfmas(a1, b1);
                 }
             }
+            PIPE_STAMP(6 + s * 5);
             if (last) {
                 prev = cur;
                 cur = nxt;
@@ -1009,6 +1056,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pipe_kernel(ConvK k, int tiles
     epilogue(prev);
 #pragma unroll
     for (int q = 0; q < C::NOUT; ++q) store_piece(q, prev);
+    PIPE_STAMP(1);
 }
 
 int g_num_cus = 0;
@@ -1068,12 +1116,322 @@ int pick_pipe(const dbsr_conv_desc* d) {
     if (d->y.ld % 8 || d->y.c0 % 8 || d->cout % 8 || (d->res.ptr && (d->res.ld % 8 || d->res.c0 % 8))) return 0;
     if (d->gate.ptr) return 0;                                   // gated (backward) convs: tiled/generic kernels
     if (cin_pad(d->cin) * 2 + 64 > ZERO_PAGE_BYTES || d->cout > 512) return 0;
+    if ((long long)d->in_h * d->in_w * d->x.ld * 2 >= (1LL << 31)) return 0;   // 32-bit buffer offsets per frame
     int cfg = 0, tw = 0, wm = 0;
     if (d->cout > 32 && d->out_w % 48 == 0) { cfg = 1; tw = 48; wm = 64; }
     else if (d->cout <= 32 && d->out_w % 64 == 0) { cfg = 2; tw = 64; wm = 32; }
     if (!cfg || d->out_h % 8) return 0;
     const long long nt = (long long)d->n_frames * (d->out_w / tw) * (d->out_h / 8) * ((d->cout + wm - 1) / wm);
     return (nt >= 256 || g_pipe_enabled == 2) ? cfg : 0;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Weight-stationary 3x3 conv for Cin <= 64 (the encoder and offset-feature ResNets and enc.out at
+// 48x48, the decoder's 64-channel pre-ResBlocks): a cout tile's weights for the whole K (9 taps x
+// Cin) fit in the registers of the four waves that use them, so only the halo moves through the LDS.
+//
+// One 256-thread block per CU, one wave per SIMD (the whole register file: weights 144 VGPRs at
+// Cin 64, accumulators in AGPRs), persistent over 16x16-pixel tiles of ONE 64-cout tile: wave
+// (wc, wp) owns couts 32wc..32wc+31 (two 16-cout MFMA blocks whose rows the packer permuted so a
+// lane ends up with 8 consecutive couts of its pixel, pipe_cout_perm) x tile rows 8wp..8wp+7.  Per
+// tile the block stages the (18 x 18)-pixel halo of all Cin channels (42 KiB at Cin 64) into one of
+// two LDS buffers by buffer-resource LDS-DMA (out-of-frame pixels land zeros); the next tile's halo,
+// the previous tile's output stores and this tile's residual loads are spread between the MFMAs, so
+// each tile costs one barrier for 288 MFMAs per wave (the pipelined kernel pays one per 108, and
+// streams the weights through the LDS with every stage).  Per (chunk, tap) step a wave reads 8
+// B-fragments (ds_read_b128) for 16 MFMAs: the LDS runs at half rate.
+// Block -> work: blockIdx % 8 is the XCD; the PX blocks of an XCD split into the nct cout tiles x
+// PX/nct spatial streams, so the cout tiles of a spatial tile (enc.out: 8) read its halo through
+// one L2.
+// ------------------------------------------------------------------------------------------------
+template <int WM, int TW, int TH, int NCH>
+struct WsCfg {
+    static constexpr int NWAVES = 8;                          // two waves per SIMD
+    static constexpr int WC = WM / 32;                        // waves across couts (32 couts each)
+    static constexpr int WP = NWAVES / WC;                    // waves across tile rows
+    static constexpr int RPW = TH / WP;                       // tile rows per wave
+    static constexpr int GPR = TW / 16;                       // 16-pixel groups per row
+    static constexpr int GW = RPW * GPR;                      // pixel groups per wave
+    static constexpr int HWD = TW + 2, HHT = TH + 2, NQ = HWD * HHT;
+    static constexpr int IN_ITEMS = (NQ + 15) / 16;           // 1-KiB halo pieces per 32-channel chunk
+    static constexpr int ITEMS = NCH * IN_ITEMS;
+    static constexpr int PER = (ITEMS + NWAVES - 1) / NWAVES; // pieces per wave per tile
+    static constexpr int STAGE_U4 = ITEMS * 64;
+    static constexpr int STEPS = NCH * 9;                     // (chunk, tap) k-steps per tile
+    static constexpr int DMA_STEPS = (STEPS + 1) / 2;         // the next halo goes out in the first half
+    static constexpr int RES_U4 = TW * TH * WM / 8;           // residual tile: [pixel][WM couts], 16-B slots
+    static constexpr int RES_ITEMS = RES_U4 / 64;             // its 1-KiB pieces (8 pixels x 128 B)
+    static constexpr int RPER = (RES_ITEMS + NWAVES - 1) / NWAVES;
+    static_assert(TH % WP == 0 && TW % 16 == 0 && WM == 64, "tile shape");
+    static_assert((2 * STAGE_U4 + 2 * RES_U4 + WM / 4) * 16 <= 160 * 1024, "halo + residual stages must fit the LDS");
+};
+
+template <typename T, int WM, int TW, int TH, int NCH, int EPI>
+__global__ __launch_bounds__(512, 1) void conv3x3_ws_kernel(ConvK k, int tiles_x, int tiles_y, int nct, int nsp,
+                                                            int px) {
+    using C = WsCfg<WM, TW, TH, NCH>;
+    static_assert(EPI >= 0 && EPI <= 3, "epilogues 0-3");
+    DBSR_OWN_SIMDS();
+    constexpr int RES_BUFS = (EPI == 0 || EPI == 2) ? 2 : 0;
+    __shared__ __attribute__((aligned(16))) u32x4_t lds[2 * C::STAGE_U4 + RES_BUFS * C::RES_U4 + WM / 4];
+    u32x4_t* lres = lds + 2 * C::STAGE_U4;                 // residual tiles (double-buffered)
+    float* lbias = (float*)(lres + RES_BUFS * C::RES_U4);  // the cout tile's bias (fp32)
+
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int g = lane >> 4, col = lane & 15;
+    const int wc = wave % C::WC, wp = wave / C::WC;
+    const bool has_res = EPI == 2 || (EPI == 0 && k.r != nullptr);
+    auto act1 = [&](float v) {
+        if constexpr (EPI == 1) return fmaxf(v, 0.f);
+        else if constexpr (EPI == 0) return apply_act(v, k.act);
+        else return v;
+    };
+    auto act2 = [&](float v) {
+        if constexpr (EPI == 2) return fmaxf(v, 0.f);
+        else if constexpr (EPI == 0) return apply_act(v, k.post_act);
+        else return v;
+    };
+
+    // block -> (cout tile, spatial stream); grid = 8 * px, px a multiple of nct
+    const int b = blockIdx.x, slot = b >> 3, spx = px / nct;
+    const int ct = slot % nct, S = 8 * spx, sid = (b & 7) * spx + slot / nct;
+    const int my_tiles = sid < nsp ? (nsp - sid + S - 1) / S : 0;
+    if (my_tiles == 0) return;
+    PIPE_STAMP(0);
+
+    // the wave's weights: A-fragments of both 16-cout blocks for every (chunk, tap), chunk-major copy
+    const int cb = ct * WM + wc * 32;
+    Frag<T> wr[NCH][9][2];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                wr[c][tap][h].load((const T*)k.w_pipe + ((((cb >> 4) + h) * NCH + c) * 9 + tap) * 512 + lane * 8);
+    if (threadIdx.x < WM) {             // ordered before its first read by the loop's first barrier
+        const int co = ct * WM + threadIdx.x;
+        lbias[threadIdx.x] = (k.bias && co < k.cout) ? k.bias[co] : 0.f;
+    }
+    const bool cout_ok = cb + 8 * g < k.cout;
+
+    struct Tile { const T* xf; long long y_off, r_off; int y0, x0; };
+    auto decode = [&](int i) {
+        int L = sid + i * S;
+        const int tx = L % tiles_x; L /= tiles_x;
+        const int ty = L % tiles_y;
+        const int f = L / tiles_y;
+        Tile t;
+        t.y0 = ty * TH; t.x0 = tx * TW;
+        t.xf = (const T*)k.x + map_frame(k.xm, f) * k.x_is;
+        const long long pix = (long long)t.y0 * k.out_w + t.x0;
+        t.y_off = map_frame(k.ym, f) * k.y_is + k.y_c0 + cb + pix * k.y_ld;
+        t.r_off = has_res ? map_frame(k.rm, f) * k.r_is + k.r_c0 + ct * WM : 0;   // frame + cout tile
+        return t;
+    };
+    // pixel of group j of this lane, relative to the tile origin
+    auto px_off = [&](int j) {
+        return (long long)(wp * C::RPW + j / C::GPR) * k.out_w + (j % C::GPR) * 16 + col;
+    };
+
+    // halo DMA: piece `it` of this wave is item wave + 4*it (clamped: surplus slots rewrite the last
+    // piece with identical bytes); lane -> (halo pixel, physical k-group slot) as in the pipelined kernel
+    const int pix_b = k.x_ld * (int)sizeof(T);
+    const unsigned frame_bytes = (unsigned)((long long)k.in_h * k.in_w * pix_b);
+    int h_rc[C::PER], h_off[C::PER];
+#pragma unroll
+    for (int it = 0; it < C::PER; ++it) {
+        const int item = min(wave + C::NWAVES * it, C::ITEMS - 1);
+        const int cch = item / C::IN_ITEMS, ii = item - cch * C::IN_ITEMS;
+        const int p = ii * 16 + (lane >> 2), ph = lane & 3;
+        const int gg = 2 * ((ph & 1) ^ ((p >> 2) & 1)) + (ph >> 1);
+        const int r = p / C::HWD, cc = p - r * C::HWD;
+        h_rc[it] = p < C::NQ ? (r << 16) | cc : 0x7fff7fff;
+        h_off[it] = (r * k.in_w + cc) * pix_b + cch * 64 + gg * 16;
+    }
+    auto dma = [&](int it, const Tile& t, int buf) {
+        const int item = min(wave + C::NWAVES * it, C::ITEMS - 1);
+        const int hy = t.y0 - 1 + (h_rc[it] >> 16), hx = t.x0 - 1 + (h_rc[it] & 0xffff);
+        const bool ok = (unsigned)hy < (unsigned)k.in_h && (unsigned)hx < (unsigned)k.in_w;
+        const int base = ((t.y0 - 1) * k.in_w + (t.x0 - 1)) * pix_b;
+        blds16(buf_rsrc(t.xf, frame_bytes), ok ? base + h_off[it] : BUF_OOB, 0, lds + buf * C::STAGE_U4 + item * 64);
+    };
+
+    // B-fragment of group j at step (chunk c, tap): halo pixel P0 + imm, k-group g (halo_phys swizzle;
+    // 8 per-lane bases cover every immediate offset)
+    const int P0 = wp * C::RPW * C::HWD + col;
+    int in_base[8];
+#pragma unroll
+    for (int rho = 0; rho < 8; ++rho) in_base[rho] = 4 * P0 + halo_phys(P0 + rho, g);
+    auto read_b = [&](const u32x4_t* lb, int step, int j) {
+        const int c = step / 9, tap = step % 9, ky = tap / 3, kx = tap % 3;
+        const int imm = (j / C::GPR + ky) * C::HWD + (j % C::GPR) * 16 + kx;
+        Frag<T> f;
+        f.v = __builtin_bit_cast(bf16x8_t, lb[c * C::IN_ITEMS * 64 + in_base[imm & 7] + 4 * imm]);
+        return f;
+    };
+
+    f32x4_t acc[2][C::GW];
+    // residual tile via LDS-DMA: piece q = 8 tile pixels x 128 B (64 couts); lane l -> pixel 8q + (l >> 3),
+    // physical slot l & 7 holding logical slot (l & 7) ^ (pixel & 7) -- the XOR keeps the epilogue's
+    // ds_read_b128 (16 consecutive pixels x 2 slots per lane group) conflict-free.  Out-of-frame bytes
+    // (a partial cout tile at the frame's last pixel) land zeros.
+    const unsigned rframe_bytes = (unsigned)((long long)k.out_h * k.out_w * k.r_ld * (int)sizeof(T));
+    auto res_dma = [&](int it, const Tile& t, int buf) {
+        const int q = min(wave + C::NWAVES * it, C::RES_ITEMS - 1);
+        const int pp = q * 8 + (lane >> 3), ls = (lane & 7) ^ (pp & 7);
+        const int off = (((t.y0 + pp / TW) * k.out_w + t.x0 + pp % TW) * k.r_ld + ls * 8) * (int)sizeof(T);
+        blds16(buf_rsrc((const T*)k.r + t.r_off, rframe_bytes), off, 0, lres + buf * C::RES_U4 + q * 64);
+    };
+    auto epilogue = [&](const Tile& t, int rbuf) {
+        const float4 b0 = *(const float4*)(lbias + wc * 32 + 8 * g);
+        const float4 b1 = *(const float4*)(lbias + wc * 32 + 8 * g + 4);
+        const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+        for (int j = 0; j < C::GW; ++j) {
+            float v[8];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                v[r] = act1(acc[0][j][r] + bv[r]);
+                v[4 + r] = act1(acc[1][j][r] + bv[4 + r]);
+            }
+            if (has_res) {
+                const int pp = (wp * C::RPW + j / C::GPR) * TW + (j % C::GPR) * 16 + col;
+                const u32x4_t rq = lres[rbuf * C::RES_U4 + pp * 8 + ((wc * 4 + g) ^ (pp & 7))];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    v[2 * e] = act2(v[2 * e] + H16<T>::lo(rq[e]));
+                    v[2 * e + 1] = act2(v[2 * e + 1] + H16<T>::hi(rq[e]));
+                }
+            }
+            u32x4_t o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = H16<T>::pack(v[2 * e], v[2 * e + 1]);
+            if (cout_ok) *(u32x4_t*)((T*)k.y + t.y_off + px_off(j) * k.y_ld + 8 * g) = o;
+        }
+    };
+
+    Tile cur = decode(0), prev = cur;
+#pragma unroll
+    for (int it = 0; it < C::PER; ++it) dma(it, cur, 0);
+    if constexpr (RES_BUFS > 0) {
+        if (has_res) {
+#pragma unroll
+            for (int it = 0; it < C::RPER; ++it) res_dma(it, cur, 0);
+        }
+    }
+
+    PIPE_STAMP(2);
+    for (int ti = 0; ti < my_tiles; ++ti) {
+        PIPE_STAMP(3 + ti * 5);
+#ifdef DBSR_PIPE_STAMPS
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        PIPE_STAMP(4 + ti * 5);
+#endif
+        __syncthreads();                // this tile's halo landed (vmcnt(0) + barrier); the other buffer is free
+        PIPE_STAMP(5 + ti * 5);
+        const bool fin = ti > 0, more = ti + 1 < my_tiles;
+        if (fin) epilogue(prev, (ti - 1) & 1);   // previous tile: accumulators + residual -> outputs
+        PIPE_STAMP(6 + ti * 5);
+        const Tile nxt = more ? decode(ti + 1) : cur;
+        const u32x4_t* lb = lds + (ti & 1) * C::STAGE_U4;
+        const int nbuf = (ti + 1) & 1;
+        Frag<T> bq[C::GW];
+#pragma unroll
+        for (int j = 0; j < C::GW; ++j) bq[j] = read_b(lb, 0, j);
+#pragma unroll
+        for (int step = 0; step < C::STEPS; ++step) {
+            // vector-memory work of this step: the next tile's halo (first half) and residual (second half;
+            // its buffer was last read by the epilogue before this tile's barrier)
+#ifndef DBSR_WS_NODMA
+            if (more) {
+#pragma unroll
+                for (int it = 0; it < C::PER; ++it)
+                    if ((it * C::DMA_STEPS) / C::PER == step) dma(it, nxt, nbuf);
+            }
+#endif
+            if constexpr (RES_BUFS > 0) {
+                if (has_res && more) {
+#pragma unroll
+                    for (int it = 0; it < C::RPER; ++it)
+                        if (C::DMA_STEPS + (it * (C::STEPS - 2 - C::DMA_STEPS)) / C::RPER == step)
+                            res_dma(it, nxt, nbuf);
+                }
+            }
+            const int c = step / 9, tap = step % 9;
+#pragma unroll
+            for (int j = 0; j < C::GW; ++j) {
+                const f32x4_t z = {0.f, 0.f, 0.f, 0.f};
+                acc[0][j] = mma(wr[c][tap][0], bq[j], step == 0 ? z : acc[0][j]);
+                acc[1][j] = mma(wr[c][tap][1], bq[j], step == 0 ? z : acc[1][j]);
+                if (step + 1 < C::STEPS) bq[j] = read_b(lb, step + 1, j);
+            }
+            // keep each B-fragment read right behind the two MFMAs that consumed its register, so it
+            // has a whole step (16 MFMAs) to land: the default schedule bunched them late
+#pragma unroll
+            for (int j = 0; j < C::GW; ++j) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);     // 2 MFMA
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);     // 1 DS read
+            }
+        }
+        PIPE_STAMP(7 + ti * 5);
+        prev = cur;
+        cur = nxt;
+    }
+    __syncthreads();                    // the last tile's residual landed
+    epilogue(prev, (my_tiles - 1) & 1);
+    PIPE_STAMP(1);
+}
+
+int g_ws_enabled = 1;
+// weight-stationary kernel for `d` (blocks per XCD, 0: not applicable): 16-bit 3x3/s1/p1/d1 with
+// 32 < cout <= 512 and 16 < cin <= 64, 16x16-divisible frames, aligned NHWC output / residual
+int pick_ws(const dbsr_conv_desc* d) {
+    if (!g_ws_enabled || !is16(d->x.dtype) || d->precise || d->kh != 3 || d->kw != 3 || d->stride != 1 ||
+        d->pad != 1 || d->dil != 1 || d->cin <= 16 || d->cin > 64 || d->out_mode != DBSR_OUT_NHWC ||
+        d->y.dtype != d->x.dtype || d->gate.ptr)
+        return 0;
+    if (d->y.ld % 8 || d->y.c0 % 8 || d->cout % 8 || d->cout <= 32 || d->cout > 512 ||
+        (d->res.ptr && (d->res.ld % 8 || d->res.c0 % 8)))
+        return 0;
+    if (d->out_w % 16 || d->out_h % 16) return 0;
+    if ((long long)d->in_h * d->in_w * d->x.ld * 2 >= (1LL << 31)) return 0;   // 32-bit buffer offsets per frame
+    const int nct = (d->cout + 63) / 64;
+    const long long nsp = (long long)d->n_frames * (d->out_w / 16) * (d->out_h / 16);
+    const int cus = d->max_blocks > 0 ? std::min(d->max_blocks, num_cus()) : num_cus();
+    const long long want = (nsp + 7) / 8;                                      // spatial streams per XCD
+    const long long spx = std::min<long long>(cus / 8 / nct, want);
+    if (spx < 1 || nsp * nct < 64) return 0;
+    return (int)(spx * nct);
+}
+
+template <typename T, int NCH>
+int launch_ws(const ConvK& k, const dbsr_conv_desc* d, int px, hipStream_t s) {
+    const int tiles_x = k.out_w / 16, tiles_y = k.out_h / 16;
+    const int nct = (k.cout + 63) / 64;
+    const int nsp = d->n_frames * tiles_x * tiles_y;
+    int epi = 0;
+    if (!k.r && k.act == DBSR_ACT_RELU) epi = 1;
+    else if (k.r && k.act == DBSR_ACT_NONE && k.post_act == DBSR_ACT_RELU) epi = 2;
+    else if (!k.r && k.act == DBSR_ACT_NONE) epi = 3;
+#define DBSR_WS_LAUNCH(E)                                                                                         \
+    hipLaunchKernelGGL((conv3x3_ws_kernel<T, 64, 16, 16, NCH, E>), dim3(8 * px), dim3(512), 0, s, k, tiles_x,    \
+                       tiles_y, nct, nsp, px)
+    switch (epi) {
+        case 1: DBSR_WS_LAUNCH(1); break;
+        case 2: DBSR_WS_LAUNCH(2); break;
+        case 3: DBSR_WS_LAUNCH(3); break;
+        default: DBSR_WS_LAUNCH(0); break;
+    }
+#undef DBSR_WS_LAUNCH
+    DBSR_LAUNCH_CHECK();
+    return 0;
+}
+
+template <typename T>
+int dispatch_ws(int px, const ConvK& k, const dbsr_conv_desc* d, hipStream_t s) {
+    if (k.CG / 4 == 1) return launch_ws<T, 1>(k, d, px, s);
+    return launch_ws<T, 2>(k, d, px, s);
 }
 
 template <typename T>
@@ -1183,6 +1541,8 @@ int dispatch_tiled_d(const ConvK& k, const dbsr_conv_desc* d, hipStream_t s) {
 template <typename T>
 int dispatch_conv(const ConvK& k, const dbsr_conv_desc* d, hipStream_t s) {
     if constexpr (sizeof(T) == 2) {
+        const int px = pick_ws(d);
+        if (px) return dispatch_ws<T>(px, k, d, s);
         const int cfg = pick_pipe(d);
         if (cfg) return dispatch_pipe<T>(cfg, k, d, s);
     }
@@ -1352,8 +1712,21 @@ ConvK make_convk(const dbsr_conv_desc* d) {
 
 }  // namespace
 
+#ifdef DBSR_PIPE_STAMPS
+extern "C" int dbsr_diag_pipe_stamps(unsigned long long* host, long long n) {
+    const long long cap = (long long)sizeof(g_pipe_stamps) / 8;
+    if (n > cap) n = cap;
+    if (!host) {
+        static unsigned long long zeros[sizeof(g_pipe_stamps) / 8];
+        return hipMemcpyToSymbol(HIP_SYMBOL(g_pipe_stamps), zeros, sizeof(zeros)) == hipSuccess ? 0 : -1;
+    }
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pipe_stamps), n * 8) == hipSuccess ? (int)n : -1;
+}
+#endif
+
 extern "C" int dbsr_conv_kernel_for(const dbsr_conv_desc* d) {
     if (!d) return -1;
+    if (pick_ws(d)) return 4;
     if (pick_pipe(d)) return 2;
     if (use_upsample(d, make_convk(d))) return 3;
     return use_tiled(d) ? 1 : 0;
@@ -1365,7 +1738,7 @@ extern "C" int dbsr_conv_head_ok(const dbsr_conv_desc* d) {
 }
 
 extern "C" size_t dbsr_conv_workspace_bytes(const dbsr_conv_desc* d) {
-    if (!d || pick_pipe(d) || use_tiled(d) || d->precise || use_upsample(d, make_convk(d))) return 0;
+    if (!d || pick_ws(d) || pick_pipe(d) || use_tiled(d) || d->precise || use_upsample(d, make_convk(d))) return 0;
     const ConvK k = make_convk(d);
     int m, n;
     pick_generic_tile(k, m, n);
@@ -1373,10 +1746,11 @@ extern "C" size_t dbsr_conv_workspace_bytes(const dbsr_conv_desc* d) {
 }
 
 extern "C" int dbsr_set_conv_algo(int algo) {
-    DBSR_CHECK_ARG(algo >= 0 && algo <= 3, "set_conv_algo: 0 generic, 1 two-barrier tiled, 2 pipelined + tiled, "
-                   "3 pipelined wherever the shape allows");
+    DBSR_CHECK_ARG(algo >= 0 && algo <= 4, "set_conv_algo: 0 generic, 1 two-barrier tiled, 2 weight-stationary + "
+                   "pipelined + tiled (default), 3 pipelined wherever the shape allows, 4 as 2 without weight-stationary");
     g_tiled_enabled = algo >= 1;
-    g_pipe_enabled = algo >= 2 ? algo - 1 : 0;
+    g_pipe_enabled = algo == 3 ? 2 : algo >= 2 ? 1 : 0;
+    g_ws_enabled = algo == 2;
     return 0;
 }
 

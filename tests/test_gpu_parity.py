@@ -163,6 +163,58 @@ def test_pipe_epilogue_variants(ops_mod, case):
     assert (outs[3] - ref).abs().mean() < 2e-3
 
 
+# (act, residual, post_act, cin, cout, dtype): the weight-stationary kernel (dbsr_conv_kernel_for == 4,
+# Cin <= 64): compile-time epilogues 1/2/3, the run-time one (LeakyReLU + residual + ReLU), one-chunk
+# Cin 32, a partial 64-cout tile (96: the second tile's upper wave has no couts), 512 couts (8 cout
+# tiles sharing a spatial tile's halo), fp16
+WS_EPI = [
+    (1, False, 0, 64, 64, torch.bfloat16), (1, False, 0, 64, 512, torch.bfloat16),
+    (0, True, 1, 64, 64, torch.bfloat16), (0, False, 0, 64, 64, torch.bfloat16),
+    (1, False, 0, 32, 64, torch.bfloat16), (0, True, 1, 64, 96, torch.bfloat16),
+    (2, True, 1, 64, 128, torch.bfloat16), (0, True, 1, 64, 64, torch.float16),
+    (1, False, 0, 48, 64, torch.float16),
+]
+
+
+@pytest.mark.parametrize('case', WS_EPI)
+def test_ws_conv_variants(ops_mod, case):
+    """Weight-stationary 3x3 conv against torch on the same 16-bit-rounded operands, and against the
+    generic kernel; frames 48x48 (the encoder's) and 32x16 (non-square, edge tiles on both axes)."""
+    from dbsr_amd import _lib
+    act, use_res, post, cin, cout, dt = case
+    for (N, H, W) in ((12, 48, 48), (40, 32, 16)):
+        gen = torch.Generator().manual_seed(cin * 13 + cout + act * 7 + post + H)
+        x = torch.randn(N, cin, H, W, generator=gen)
+        w = torch.randn(cout, cin, 3, 3, generator=gen) / (cin * 9) ** 0.5
+        b = torch.randn(cout, generator=gen) * 0.1
+        res = torch.randn(N, cout, H, W, generator=gen) if use_res else None
+        xb, wb = x.to(dt).float(), w.to(dt).float()
+        ref = F.conv2d(xb, wb, b, padding=1)
+        if act == 1:
+            ref = F.relu(ref)
+        elif act == 2:
+            ref = F.leaky_relu(ref, 0.1)
+        if use_res:
+            ref = ref + res.to(dt).float()
+        if post:
+            ref = F.relu(ref)
+        outs = {}
+        try:
+            for algo in (2, 0):
+                _lib.lib().dbsr_set_conv_algo(algo)
+                outs[algo] = ops_mod.conv2d(x.to(DEV), w.to(DEV), b.to(DEV), padding=1, act=act,
+                                            residual=res.to(DEV) if use_res else None, post_act=post,
+                                            compute_dtype=dt).float().cpu()
+                if algo == 2:
+                    assert ops_mod.conv2d.last_kernel == 4, (N, H, W, ops_mod.conv2d.last_kernel)
+        finally:
+            _lib.lib().dbsr_set_conv_algo(2)
+        # 16-bit output: one rounding of the fp32 result (bf16 2^-8, fp16 2^-11 relative)
+        np.testing.assert_allclose(outs[2].numpy(), ref.numpy(), atol=2e-2, rtol=1e-2)
+        np.testing.assert_allclose(outs[2].numpy(), outs[0].numpy(), atol=2e-2, rtol=1e-2)
+        assert (outs[2] - ref).abs().mean() < 2e-3
+
+
 @pytest.fixture(scope='module')
 def ops_mod():
     from dbsr_amd import ops as O

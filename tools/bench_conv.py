@@ -55,7 +55,7 @@ def main():
         for algo in algos:
             L.lib().dbsr_set_conv_algo(algo)
             ms = plan.time_ops(s, reps=args.reps)[0][1]
-            out.append('%s %7.1f us %6.1f TF/s' % (['generic', 'tiled', 'auto', 'pipe'][algo], ms * 1e3, flop / ms / 1e9))
+            out.append('%s %7.1f us %6.1f TF/s' % (['generic', 'tiled', 'auto', 'pipe', 'no-ws'][algo], ms * 1e3, flop / ms / 1e9))
         L.lib().dbsr_set_conv_algo(2)
         print(f'{name:22s} ' + ' | '.join(out))
 
