@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get('DBSR_HIP_LIB', os.path.join(_HERE, 'libdbsr_hip.so'))
 DBSR_F32, DBSR_BF16, DBSR_F16 = 0, 1, 2
 ACT_NONE, ACT_RELU, ACT_LRELU = 0, 1, 2
 OUT_NHWC, OUT_SHUFFLE, OUT_NCHW_F32 = 0, 1, 2
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 
 class FrameMap(ctypes.Structure):
@@ -107,6 +107,12 @@ def lib():
             'dbsr_adam_step': ([c_ll, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_float, c_float, c_float, c_int,
                                 c_float, c_void_p], c_int),
             'dbsr_dgrad_weights': ([c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p], c_int),
+            'dbsr_resize_bilinear': ([c_int, c_int, c_int, c_void_p, c_int, c_int, c_float, c_float, c_float, c_void_p,
+                                      c_void_p], c_int),
+            'dbsr_gauss_reflect': ([c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
+            'dbsr_color_fit': ([c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
+            'dbsr_color_apply': ([c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_int,
+                                  c_int, c_float, c_float, c_void_p, c_void_p, c_void_p], c_int),
         }
         for name, (args, res) in sigs.items():
             fn = getattr(L, name)
@@ -127,7 +133,8 @@ EXPORTED = ['dbsr_abi_version', 'dbsr_last_error', 'dbsr_conv_packed_elems', 'db
             'dbsr_merge_prep', 'dbsr_pwc_assemble', 'dbsr_zero', 'dbsr_conv_wgrad_workspace_bytes', 'dbsr_conv_wgrad',
             'dbsr_chan_sum_workspace_bytes', 'dbsr_chan_sum', 'dbsr_l1_loss_backward', 'dbsr_unshuffle_gate',
             'dbsr_fuse_backward', 'dbsr_merge_prep_backward', 'dbsr_warp_backward', 'dbsr_enc_grad_gate',
-            'dbsr_adam_step', 'dbsr_dgrad_weights']
+            'dbsr_adam_step', 'dbsr_dgrad_weights',
+            'dbsr_resize_bilinear', 'dbsr_gauss_reflect', 'dbsr_color_fit', 'dbsr_color_apply']
 
 
 def check(rc, what):

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DBSR_ABI_VERSION 7
+#define DBSR_ABI_VERSION 8
 
 enum { DBSR_F32 = 0, DBSR_BF16 = 1, DBSR_F16 = 2 };
 enum { DBSR_ACT_NONE = 0, DBSR_ACT_RELU = 1, DBSR_ACT_LRELU = 2 };      /* LeakyReLU slope 0.1 */
@@ -193,6 +193,24 @@ int dbsr_merge_prep(int B, int N, int hw, int c, dbsr_tensor proj, dbsr_tensor o
  * writes first/flow/feat into out channels [c0+81, c0+81+C+4). first: map pair->ref frame. */
 int dbsr_pwc_assemble(int n_pairs, int h, int w, int c, dbsr_tensor first, dbsr_tensor flow,
                       dbsr_tensor feat, dbsr_tensor out, void* stream);
+
+/* ---------------- BurstSR scoring: SpatialColorAlignment (spatial_color_alignment.py:23-108) ----------------
+ * fp32 NCHW planes.  rh / rw are PyTorch's internal source-coordinate ratios, 1 / scale_factor. */
+/* F.interpolate(bilinear, align_corners=False, scale_factor) of `planes` planes, times mul
+ * (spatial_color_alignment.py:96-101: flow_ds = interpolate(flow, 1/8) * 1/8, frame_gt_ds). */
+int dbsr_resize_bilinear(int planes, int ih, int iw, const float* in, int oh, int ow, float rh, float rw, float mul,
+                         float* out, void* stream);
+/* apply_kernel (filtering.py:56-63): reflect padding + ksz x ksz filter (k_host: ksz*ksz floats, ksz odd <= 9). */
+int dbsr_gauss_reflect(int planes, int h, int w, int ksz, const float* k_host, const float* in, float* out,
+                       void* stream);
+/* match_colors' least squares (spatial_color_alignment.py:36-44): per image, C[3][3] minimising
+ * ||Q C - R|| over the [bi, h-bi) x [bi, w-bi) crop of the smoothed images ref (R) and q (Q). */
+int dbsr_color_fit(int n, int h, int w, int bi, const float* ref, const float* q, float* c_mat, void* stream);
+/* match_colors' transform + validity mask (spatial_color_alignment.py:45-67): out = test^T C per pixel,
+ * valid (uint8) = bilinear-upsampled (err < thresh on the crop, 0 in the bi border) > 0.9. */
+int dbsr_color_apply(int n, int h, int w, int bi, const float* ref, const float* q, const float* c_mat, float thresh,
+                     const float* test, int oh, int ow, float rh, float rw, float* out, unsigned char* valid,
+                     void* stream);
 
 /* ---------------- training step (BASELINE configs[3]; trainers/simple_trainer.py:78-81) ----------------
  * Backward of the DBSR part (PWC-Net is frozen, encoders.py:56-61).  Conv dgrad = dbsr_conv2d with the

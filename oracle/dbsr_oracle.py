@@ -333,3 +333,59 @@ def dbsr_forward(burst, sd, kw=DBSR_SYNTHETIC_KWARGS, zero_flow=False, return_in
 
 def state_dict_to_torch(sd_np, dtype=torch.float32):
     return {k: torch.from_numpy(v).to(dtype) for k, v in sd_np.items()}
+
+
+# ----------------------------------------------------------------------------------------------
+# BurstSR scoring: SpatialColorAlignment (models/loss/spatial_color_alignment.py:23-108)
+# ----------------------------------------------------------------------------------------------
+def gaussian_kernel_2d(sd, ksz=None):
+    """get_gaussian_kernel (filtering.py:20-51): normalised density on an odd ksz grid."""
+    if ksz is None:
+        ksz = int(4 * sd + 1)
+    k = torch.arange(-(ksz - 1) / 2, (ksz + 1) / 2).reshape(1, -1)
+    g = torch.exp(-1.0 / (2 * sd ** 2) * (k - torch.zeros(1, 1)) ** 2) / (math.sqrt(2 * math.pi) * sd)
+    K = g.reshape(1, 1, -1) * g.reshape(1, -1, 1)
+    return (K / K.sum()), ksz
+
+
+def apply_kernel(im, ksz, kernel):
+    """filtering.py:54-63."""
+    shape = im.shape
+    im = im.reshape(-1, 1, *im.shape[-2:])
+    im = F.pad(im, [ksz // 2] * 4, mode='reflect')
+    return F.conv2d(im, kernel.unsqueeze(0).to(im.dtype)).view(shape)
+
+
+def match_colors(im_ref, im_q, im_test, ksz, gauss_kernel, bi=5, thresh=20):
+    """spatial_color_alignment.py:23-67; torch.lstsq(B, A) (removed in torch 2.x) is its least-squares
+    solution of A X = B, torch.linalg.lstsq here.  Returns (im_test^T C, valid, C)."""
+    ref_m = apply_kernel(im_ref, ksz, gauss_kernel)[:, :, bi:-bi, bi:-bi].contiguous()
+    q_m = apply_kernel(im_q, ksz, gauss_kernel)[:, :, bi:-bi, bi:-bi].contiguous()
+    ref_re = ref_m.view(*ref_m.shape[:2], -1)
+    q_re = q_m.view(*q_m.shape[:2], -1)
+    c_mat = torch.stack([torch.linalg.lstsq(iq.t(), ir.t()).solution[:3] for ir, iq in zip(ref_re, q_re)], 0)
+    q_conv = torch.matmul(q_re.permute(0, 2, 1), c_mat).permute(0, 2, 1).view(q_m.shape)
+    err = ((q_conv - ref_m) * 255.0).norm(dim=1)
+    valid = err < thresh
+    pad = (im_q.shape[-1] - valid.shape[-1]) // 2
+    valid = F.pad(valid, [pad] * 4)
+    f = im_test.shape[-1] / valid.shape[-1]
+    valid = F.interpolate(valid.unsqueeze(1).float(), scale_factor=f, mode='bilinear') > 0.9
+    t_re = im_test.view(*im_test.shape[:2], -1)
+    out = torch.matmul(t_re.permute(0, 2, 1), c_mat).permute(0, 2, 1).view(im_test.shape)
+    return out, valid, c_mat
+
+
+def spatial_color_alignment(pred, gt, burst_input, sd, sr_factor=4, p='encoder.alignment_net.net'):
+    """SpatialColorAlignment.forward (spatial_color_alignment.py:87-108) with the oracle PWC-Net.
+    Returns (pred_warped_m, valid, flow, c_mat)."""
+    flow = pwcnet(pred / (pred.max() + 1e-6), gt / (gt.max() + 1e-6), sd, p)
+    pred_warped = warp(pred, flow)
+    ds = 1.0 / float(2.0 * sr_factor)
+    flow_ds = F.interpolate(flow, scale_factor=ds, mode='bilinear') * ds
+    burst_0 = burst_input[:, 0, [0, 1, 3]].contiguous()
+    burst_0_warped = warp(burst_0, flow_ds)
+    gt_ds = F.interpolate(gt, scale_factor=ds, mode='bilinear')
+    K, ksz = gaussian_kernel_2d(1.5)
+    out, valid, c_mat = match_colors(gt_ds, burst_0_warped, pred_warped, ksz, K)
+    return out, valid, flow, c_mat
