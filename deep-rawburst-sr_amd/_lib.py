@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get('DBSR_HIP_LIB', os.path.join(_HERE, 'libdbsr_hip.so'))
 DBSR_F32, DBSR_BF16, DBSR_F16 = 0, 1, 2
 ACT_NONE, ACT_RELU, ACT_LRELU = 0, 1, 2
 OUT_NHWC, OUT_SHUFFLE, OUT_NCHW_F32 = 0, 1, 2
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 
 class FrameMap(ctypes.Structure):
@@ -29,6 +29,12 @@ IDENTITY = (1, 1, 0, 1)
 class Tensor(ctypes.Structure):
     _fields_ = [('ptr', ctypes.c_void_p), ('dtype', ctypes.c_int), ('img_stride', ctypes.c_longlong),
                 ('ld', ctypes.c_int), ('c0', ctypes.c_int), ('map', FrameMap)]
+
+
+class PwcDenseConv(ctypes.Structure):
+    """dbsr_pwc_dense_conv (include/dbsr_hip.h)."""
+    _fields_ = [('w', ctypes.c_void_p), ('bias', ctypes.c_void_p), ('kp', ctypes.c_int), ('cg', ctypes.c_int),
+                ('start', ctypes.c_int), ('cout', ctypes.c_int), ('out_off', ctypes.c_int)]
 
 
 class ConvDesc(ctypes.Structure):
@@ -107,6 +113,8 @@ def lib():
             'dbsr_adam_step': ([c_ll, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_float, c_float, c_float, c_int,
                                 c_float, c_void_p], c_int),
             'dbsr_dgrad_weights': ([c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p], c_int),
+            'dbsr_pwc_dense': ([c_int, c_int, c_int, Tensor, c_int, c_void_p, Tensor, c_void_p], c_int),
+            'dbsr_pwc_dense_supported': ([c_int, c_int, c_int], c_int),
             'dbsr_resize_bilinear': ([c_int, c_int, c_int, c_void_p, c_int, c_int, c_float, c_float, c_float, c_void_p,
                                       c_void_p], c_int),
             'dbsr_gauss_reflect': ([c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
@@ -134,7 +142,8 @@ EXPORTED = ['dbsr_abi_version', 'dbsr_last_error', 'dbsr_conv_packed_elems', 'db
             'dbsr_chan_sum_workspace_bytes', 'dbsr_chan_sum', 'dbsr_l1_loss_backward', 'dbsr_unshuffle_gate',
             'dbsr_fuse_backward', 'dbsr_merge_prep_backward', 'dbsr_warp_backward', 'dbsr_enc_grad_gate',
             'dbsr_adam_step', 'dbsr_dgrad_weights',
-            'dbsr_resize_bilinear', 'dbsr_gauss_reflect', 'dbsr_color_fit', 'dbsr_color_apply']
+            'dbsr_resize_bilinear', 'dbsr_gauss_reflect', 'dbsr_color_fit', 'dbsr_color_apply', 'dbsr_pwc_dense',
+            'dbsr_pwc_dense_supported']
 
 
 def check(rc, what):

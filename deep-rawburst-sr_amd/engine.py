@@ -273,6 +273,7 @@ def _param_signature(module):
 # ==================================================================================================
 class PWCPlanner:
     """Packs PWC-Net weights and emits the PWC part of a plan (pwcnet.py:221-231 + :262-279)."""
+    FUSED_DENSE = True        # 16-bit coarse levels (<= 64 pixels per pair): dbsr_pwc_dense
     def __init__(self, pwc_module, W):
         net = pwc_module.net
         ex = net.netExtractor
@@ -342,14 +343,30 @@ class PWCPlanner:
                 plan.keep.extend([fu, fe, ws])
             plan.add(f'pwc.dec{level}.corr', lib.dbsr_correlation, P, h, w, C, feat.d(0, first_map), second,
                      D.d(BASE_OFF), 1)
-            cin = base_real
-            for i, (pc, off) in enumerate(zip(ent['dense'], DENSE_OFF)):
-                start = BASE_OFF if i == 0 else DENSE_OFF[i - 1]
-                plan.conv(f'pwc.dec{level}.dense{i}', pc, P, D, start, (h, w), D, off, L.ACT_LRELU, cin=cin)
-                cin += DENSE_OUT[i]
             fl = NHWC(P, h, w, 8, torch.float32, device)    # 2 ch (ld 8: read by the next level's ConvT)
-            plan.conv(f'pwc.dec{level}.flow', ent['flow'], P, D, 0, (h, w), None, 0, L.ACT_NONE, cin=cin,
-                      y_desc=fl.d(0))
+            if PWCPlanner.FUSED_DENSE and dtype != torch.float32 and lib.dbsr_pwc_dense_supported(h, w, ld):
+                # coarse level: the DenseNet + flow conv in one launch with D in LDS (csrc/pwc_dense.hip)
+                convs = (L.PwcDenseConv * 6)()
+                cin, flop = base_real, 0.0
+                for i, pc in enumerate(ent['dense'] + [ent['flow']]):
+                    start = 0 if i == 5 else (BASE_OFF if i == 0 else DENSE_OFF[i - 1])
+                    cg = cpad(pc.cin) // 8
+                    convs[i] = L.PwcDenseConv(pc.w.data_ptr(), pc.bias.data_ptr() if pc.bias is not None else None,
+                                              9 * cg * 8, cg, start, pc.cout, DENSE_OFF[i] if i < 5 else 0)
+                    flop += 2.0 * P * h * w * pc.cout * pc.cin * 9
+                plan.keep.append(convs)
+                plan.add(f'pwc.dec{level}.dense', lib.dbsr_pwc_dense, P, h, w, D.d(0), BASE_OFF, convs, fl.d(0),
+                         work=('flop', flop))
+                plan.kernel[len(plan.ops) - 1] = 'pwc_dense'
+                cin = base_real + sum(DENSE_OUT)
+            else:
+                cin = base_real
+                for i, (pc, off) in enumerate(zip(ent['dense'], DENSE_OFF)):
+                    start = BASE_OFF if i == 0 else DENSE_OFF[i - 1]
+                    plan.conv(f'pwc.dec{level}.dense{i}', pc, P, D, start, (h, w), D, off, L.ACT_LRELU, cin=cin)
+                    cin += DENSE_OUT[i]
+                plan.conv(f'pwc.dec{level}.flow', ent['flow'], P, D, 0, (h, w), None, 0, L.ACT_NONE, cin=cin,
+                          y_desc=fl.d(0))
             plan.keep.extend([D, fl])
             prev = (D, fl, base_real)
         # ---- refiner (pwcnet.py:186-207) + residual flow (:231) ----
@@ -370,6 +387,7 @@ class PWCPlanner:
 # DBSR engine
 # ==================================================================================================
 class DBSREngine:
+    LANE0_CU_SHARE = 0.5      # CU share of lane 0's persistent convs while the PWC lane runs (tools/capbench.sh)
     # bf16: fuse the RGB predictor into the last decoder ResBlock conv (False: separate fp32 kernel)
     FUSED_HEAD = True
 
@@ -463,7 +481,8 @@ class DBSREngine:
         # (large launches); they meet at the warp.
         plan.fork(1, dev, priority=-1)
         # while the side lane runs, lane-0 persistent convs leave a quarter of the CUs to it
-        plan_cap = torch.cuda.get_device_properties(dev).multi_processor_count * 3 // 4 if Plan.MULTI_STREAM else 0
+        plan_cap = int(torch.cuda.get_device_properties(dev).multi_processor_count * DBSREngine.LANE0_CU_SHARE) \
+            if Plan.MULTI_STREAM else 0
         # ---------------- alignment (PWC-Net) ----------------
         if not zero_flow:
             flow_out = NHWC(P, Hp // 4, Wp // 4, 2, torch.float32, dev)

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DBSR_ABI_VERSION 8
+#define DBSR_ABI_VERSION 9
 
 enum { DBSR_F32 = 0, DBSR_BF16 = 1, DBSR_F16 = 2 };
 enum { DBSR_ACT_NONE = 0, DBSR_ACT_RELU = 1, DBSR_ACT_LRELU = 2 };      /* LeakyReLU slope 0.1 */
@@ -193,6 +193,22 @@ int dbsr_merge_prep(int B, int N, int hw, int c, dbsr_tensor proj, dbsr_tensor o
  * writes first/flow/feat into out channels [c0+81, c0+81+C+4). first: map pair->ref frame. */
 int dbsr_pwc_assemble(int n_pairs, int h, int w, int c, dbsr_tensor first, dbsr_tensor flow,
                       dbsr_tensor feat, dbsr_tensor out, void* stream);
+
+/* Fused PWC decoder DenseNet of one coarse level (pwcnet.py:153-184, levels with <= 64 pixels per
+ * pair): the five LeakyReLU dense convs and the flow conv over D [P][h][w][ld] (16-bit; base channels
+ * already assembled), dense outputs written into D's channels [0, dense_ch), flow (fp32, 2 ch) to flow.
+ * convs[0..4]: dense, convs[5]: flow; weights packed by dbsr_conv_pack_weights (3x3, cin > 16). */
+typedef struct {
+    const void* w;
+    const float* bias;
+    int kp, cg;          /* packed K (= 9 * cg * 8) and 8-channel input groups per tap (cg % 4 == 0) */
+    int start;           /* first input channel in D */
+    int cout, out_off;   /* output channels, their offset in D (ignored for the flow conv) */
+} dbsr_pwc_dense_conv;
+int dbsr_pwc_dense(int P, int h, int w, dbsr_tensor D, int dense_ch, const dbsr_pwc_dense_conv* convs,
+                   dbsr_tensor flow, void* stream);
+/* 1 if dbsr_pwc_dense has an LDS tile for an h x w level with ld channels in D (else use dbsr_conv2d). */
+int dbsr_pwc_dense_supported(int h, int w, int ld);
 
 /* ---------------- BurstSR scoring: SpatialColorAlignment (spatial_color_alignment.py:23-108) ----------------
  * fp32 NCHW planes.  rh / rw are PyTorch's internal source-coordinate ratios, 1 / scale_factor. */

@@ -281,3 +281,38 @@ def test_cfg5_frame_sharded_4_ranks_fp16(cfg4_case):
     print('fp16 x16 4-rank frame-sharded: PSNR delta %.5f dB' % dp)
     assert pred.shape == (1, 3, 1536, 1536)
     assert dp <= 0.01
+
+
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
+def test_pwc_fused_dense_levels(synth_sd, dtype):
+    """The fused coarse-level DenseNet (dbsr_pwc_dense, levels 6..3) against the per-conv path on the same
+    16-bit inputs, and both against the fp32 oracle PWC-Net (pwcnet.py:248-281): the fused path may not
+    be further from the oracle than the per-conv one (the two differ only in summation order and in
+    where activations round to 16 bits)."""
+    from dbsr_amd.engine import PWCPlanner
+    from dbsr_amd.pwcnet import PWCNet
+    from oracle import dbsr_oracle as orc
+    pre = 'encoder.alignment_net.'
+    gen = torch.Generator().manual_seed(5)
+    src = torch.rand(6, 3, 96, 80, generator=gen)
+    tgt = (src + 0.05 * torch.randn(6, 3, 96, 80, generator=gen)).clamp(0, 1)
+    ref = orc.pwcnet(src, tgt, synth_sd)
+    flows = {}
+    try:
+        for fused in (True, False):
+            PWCPlanner.FUSED_DENSE = fused
+            net = PWCNet(load_pretrained=False)
+            net.load_state_dict({k[len(pre):]: v for k, v in synth_sd.items() if k.startswith(pre)})
+            net = net.to(DEV)
+            net.compute_dtype = dtype
+            with torch.no_grad():
+                flows[fused] = net(src.to(DEV), tgt.to(DEV)).cpu()
+    finally:
+        PWCPlanner.FUSED_DENSE = True
+    e_f = (flows[True] - ref).abs().max().item()
+    e_u = (flows[False] - ref).abs().max().item()
+    d = (flows[True] - flows[False]).abs().max().item()
+    scale = ref.abs().max().item()
+    print('fused err %.4g unfused err %.4g diff %.4g (|flow| max %.3g)' % (e_f, e_u, d, scale))
+    assert e_f <= max(1.5 * e_u, 2e-3 * scale)
+    assert d <= 0.02 * scale
