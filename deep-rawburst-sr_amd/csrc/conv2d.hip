@@ -1226,7 +1226,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ws_kernel(ConvK k, int tiles_x
         t.xf = (const T*)k.x + map_frame(k.xm, f) * k.x_is;
         const long long pix = (long long)t.y0 * k.out_w + t.x0;
         t.y_off = map_frame(k.ym, f) * k.y_is + k.y_c0 + cb + pix * k.y_ld;
-        t.r_off = has_res ? map_frame(k.rm, f) * k.r_is + k.r_c0 + ct * WM : 0;   // frame + cout tile
+        t.r_off = has_res ? map_frame(k.rm, f) * k.r_is : 0;   // residual frame base (buffer-resource base)
         return t;
     };
     // pixel of group j of this lane, relative to the tile origin
@@ -1276,11 +1276,14 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ws_kernel(ConvK k, int tiles_x
     // physical slot l & 7 holding logical slot (l & 7) ^ (pixel & 7) -- the XOR keeps the epilogue's
     // ds_read_b128 (16 consecutive pixels x 2 slots per lane group) conflict-free.  Out-of-frame bytes
     // (a partial cout tile at the frame's last pixel) land zeros.
+    // the resource spans the residual frame from its first channel, so the slots of a partial cout tile
+    // past the frame's last pixel fall outside it (zeros) rather than past the allocation
     const unsigned rframe_bytes = (unsigned)((long long)k.out_h * k.out_w * k.r_ld * (int)sizeof(T));
+    const int r_cb = k.r_c0 + ct * WM;
     auto res_dma = [&](int it, const Tile& t, int buf) {
         const int q = min(wave + C::NWAVES * it, C::RES_ITEMS - 1);
         const int pp = q * 8 + (lane >> 3), ls = (lane & 7) ^ (pp & 7);
-        const int off = (((t.y0 + pp / TW) * k.out_w + t.x0 + pp % TW) * k.r_ld + ls * 8) * (int)sizeof(T);
+        const int off = (((t.y0 + pp / TW) * k.out_w + t.x0 + pp % TW) * k.r_ld + r_cb + ls * 8) * (int)sizeof(T);
         blds16(buf_rsrc((const T*)k.r + t.r_off, rframe_bytes), off, 0, lres + buf * C::RES_U4 + q * 64);
     };
     auto epilogue = [&](const Tile& t, int rbuf) {

@@ -292,10 +292,10 @@ class PWCPlanner:
             self.dec[level] = ent
         self.ref = [W.conv(net.netRefiner.netMain[i]) for i in range(0, 13, 2)]
 
-    def build(self, plan, dtype, device, nF, Hp, Wp, P, first_map, second_map, rgb, flow_out):
-        """Emit: extractor over the nF frames stored in `rgb` ([nF,Hp,Wp,8]); decoders over P pairs whose
-        first/second features are frames first_map(p) / second_map(p); refined flow (fp32, 2 ch) into
-        `flow_out` ([P,Hp/4,Wp/4,2])."""
+    def build(self, plan, dtype, device, nF, Hp, Wp, P, first_map, second_map, rgb, flow_out, rgb_map=IDENTITY):
+        """Emit: extractor over the nF frames rgb_map(0..nF-1) of `rgb` ([*,Hp,Wp,8]); decoders over P pairs
+        whose first/second features are frames first_map(p) / second_map(p) of the extractor's outputs;
+        refined flow (fp32, 2 ch) into `flow_out` ([P,Hp/4,Wp/4,2])."""
         lib = L.lib()
         # ---- feature pyramid (Extractor.forward, pwcnet.py:103-111), once per frame ----
         levels = {}
@@ -306,7 +306,8 @@ class PWCPlanner:
             ta = NHWC(nF, oh, ow, cpad(C), dtype, device)
             tb = NHWC(nF, oh, ow, cpad(C), dtype, device)
             lv = NHWC(nF, oh, ow, cpad(C), dtype, device)
-            plan.conv(f'pwc.ext{k + 1}.0', self.ext[k][0], nF, x, 0, hw, ta, 0, L.ACT_LRELU)
+            plan.conv(f'pwc.ext{k + 1}.0', self.ext[k][0], nF, x, 0, hw, ta, 0, L.ACT_LRELU,
+                      xmap=rgb_map if k == 0 else IDENTITY)
             plan.conv(f'pwc.ext{k + 1}.2', self.ext[k][1], nF, ta, 0, (oh, ow), tb, 0, L.ACT_LRELU)
             plan.conv(f'pwc.ext{k + 1}.4', self.ext[k][2], nF, tb, 0, (oh, ow), lv, 0, L.ACT_LRELU)
             levels[k + 1] = lv
@@ -388,6 +389,9 @@ class PWCPlanner:
 # ==================================================================================================
 class DBSREngine:
     LANE0_CU_SHARE = 0.5      # CU share of lane 0's persistent convs while the PWC lane runs (tools/capbench.sh)
+    PIPELINE_GROUPS = 1       # burst groups (alignment of group g+1 beside merge + decoder of g): 2 measured
+                              # 2037 vs 2388 bursts/s at configs[1] -- the PWC chain is latency-bound, so two
+                              # half-batch chains take twice as long (tools/sweep_engine.py)
     # bf16: fuse the RGB predictor into the last decoder ResBlock conv (False: separate fp32 kernel)
     FUSED_HEAD = True
 
@@ -455,17 +459,96 @@ class DBSREngine:
             a = c
         return (a, fused) if head is not None else a
 
+    def _groups(self, B, mode):
+        """Burst groups of the software pipeline: the alignment chain of group g+1 (PWC-Net + offset-feature
+        extractor: many small latency-bound launches) runs on the side lane while lane 0 runs the merge +
+        decoder of group g.  One group for mode 'partial' and for B == 1."""
+        G = min(B, DBSREngine.PIPELINE_GROUPS) if mode == 'full' else 1
+        bounds = [(i * B) // G for i in range(G + 1)]
+        return [(bounds[i], bounds[i + 1]) for i in range(G)]
+
+    def _emit_align(self, plan, grp, N, H, W, sh):
+        """PWC-Net flow of the group's pairs -> offsets / offset features (flow_finalize) -> offset-feature
+        extractor (merging.py:85-87) -> WP[..., 2*pd:] of the group."""
+        dt, dev = self.dtype, self.device
+        lib = L.lib()
+        g0, g1 = grp
+        Bg, Fg, Pg = g1 - g0, (g1 - g0) * N, (g1 - g0) * (N - 1)
+        off_f, off_p = g0 * N, g0 * (N - 1)
+        Hp, Wp = sh['Hp'], sh['Wp']
+        hw = (H, W)
+        fmap = (1, 1, off_f, 0)                       # frame f of the group -> frame off_f + f of the batch
+        if not self.zero_flow:
+            flow_out = NHWC(Pg, Hp // 4, Wp // 4, 2, torch.float32, dev)
+            self.pwc.build(plan, dt, dev, Fg, Hp, Wp, Pg, first_map=(N - 1, N, 0, 0), second_map=(N - 1, N, 1, 1),
+                           rgb=sh['rgb'], flow_out=flow_out, rgb_map=fmap)
+            plan.add('flow_finalize', lib.dbsr_flow_finalize, Bg, N, Hp // 4, Wp // 4, flow_out.d(0), H, W, Hp, Wp,
+                     sh['offsets'][off_p:].data_ptr(), 1.0, sh['om'].d(0, fmap))
+            plan.keep.append(flow_out)
+        # (zero flow: offsets and om stay zero from initialisation)
+        pd, od = self.proj.cout, self.ofe_init.cout
+        WP = NHWC(Fg, H, W, 2 * pd + od, dt, dev)
+        o = [NHWC(Fg, H, W, od, dt, dev) for _ in range(3)]
+        plan.conv('merge.ofe.init', self.ofe_init, Fg, sh['om'], 0, hw, o[0], 0, L.ACT_RELU, xmap=fmap)
+        a = 0
+        if not self.ofe_res:
+            raise NotImplementedError('num_offset_feat_extractor_res must be >= 1')
+        for k, (c1, c2) in enumerate(self.ofe_res):
+            b, c = [j for j in range(3) if j != a]
+            last = k == len(self.ofe_res) - 1
+            plan.conv(f'merge.ofe.res{k}.conv1', c1, Fg, o[a], 0, hw, o[b], 0, L.ACT_RELU)
+            if last:
+                plan.conv(f'merge.ofe.res{k}.conv2', c2, Fg, o[b], 0, hw, WP, 2 * pd, L.ACT_NONE, res=o[a],
+                          post_act=L.ACT_RELU)
+            else:
+                plan.conv(f'merge.ofe.res{k}.conv2', c2, Fg, o[b], 0, hw, o[c], 0, L.ACT_NONE, res=o[a],
+                          post_act=L.ACT_RELU)
+                a = c
+        plan.keep.extend([WP, o])
+        return WP
+
+    def _emit_merge(self, plan, grp, N, H, W, sh, WP):
+        """Warp (encoders.py:80) + projections, weight predictor (merging.py:61-113) of the group; returns
+        the logits LG and the warped embeddings Wf."""
+        dt, dev = self.dtype, self.device
+        lib = L.lib()
+        g0, g1 = grp
+        Bg, Fg, Pg = g1 - g0, (g1 - g0) * N, (g1 - g0) * (N - 1)
+        off_f, off_p = g0 * N, g0 * (N - 1)
+        C, E, PJ = self.enc_out.cout, sh['E'], sh['PJ']
+        hw = (H, W)
+        pd = self.proj.cout
+        Wf = NHWC(max(Pg, 1), H, W, C, dt, dev)
+        es = 4 if dt == torch.float32 else 2
+        if Pg > 0:
+            plan.add('warp', lib.dbsr_warp_bilinear, Pg, H, W, C, E.d(0, (N - 1, N, 1 + off_f, 1)),
+                     sh['offsets'][off_p:].data_ptr(), 2 * H * W, Wf.d(0),
+                     work=('byte', 2.0 * Pg * C * H * W * es + 8.0 * Pg * H * W))
+            plan.conv('merge.proj_oth', self.proj, Pg, Wf, 0, hw, PJ, 0, L.ACT_RELU, ymap=(N - 1, N, 1 + off_f, 1))
+        plan.add('merge.prep', lib.dbsr_merge_prep, Bg, N, H * W, pd, PJ.d(0, (1, 1, off_f, 0)), WP.d(0))
+        q = [NHWC(Fg, H, W, self.wp_init.cout, dt, dev) for _ in range(3)]
+        plan.conv('merge.wp.init', self.wp_init, Fg, WP, 0, hw, q[0], 0, L.ACT_RELU)
+        i = self._resblocks(plan, 'merge.wp.res', self.wp_res, Fg, hw, q, 0, dt)
+        LG = NHWC(Fg, H, W, C, dt, dev)
+        plan.conv('merge.wp.out', self.wp_out, Fg, q[i], 0, hw, LG, 0, L.ACT_NONE)
+        plan.keep.extend([Wf, q, LG])
+        return LG, Wf
+
     def _build(self, B, N, H, W, mode='full', first_frame=0):
         """mode 'full': the whole forward.  mode 'partial' (frame-sharded fusion): stop after
         the weight predictor and emit dbsr_fuse_partial statistics of frames [first_frame, N) into
-        bufs['stats'] instead of the fusion and the decoder (those run in `_build_combine`)."""
+        bufs['stats'] instead of the fusion and the decoder (those run in `_build_combine`).
+
+        Lanes: the alignment chain of a burst group (PWC-Net, flow finalize, offset-feature extractor)
+        runs on side lane 1; lane 0 runs the encoder over the whole batch, then per group waits for that
+        group's alignment and runs its merge + fusion + decoder while lane 1 already aligns the next group
+        (`_groups`).  Single-stream mode issues the same launches in the same order on one stream."""
         dt, dev = self.dtype, self.device
         lib = L.lib()
         plan = Plan()
         F, P = B * N, B * (N - 1)
         C = self.enc_out.cout
         hw = (H, W)
-        S = self.s
         bufs = {}
         bufs['burst'] = torch.zeros(B, N, 4, H, W, dtype=torch.float32, device=dev)
         raw = NHWC(F, H, W, 8, dt, dev)
@@ -473,101 +556,68 @@ class DBSREngine:
         rgb = NHWC(F, Hp, Wp, 8, dt, dev)
         bufs['offsets'] = torch.zeros(P, 2, H, W, dtype=torch.float32, device=dev)
         om = NHWC(F, H, W, 8, dt, dev)
-        zero_flow = self.zero_flow
+        E = NHWC(F, H, W, C, dt, dev)
+        PJ = NHWC(F, H, W, r8(self.proj.cout), dt, dev)
+        sh = {'rgb': rgb, 'offsets': bufs['offsets'], 'om': om, 'E': E, 'PJ': PJ, 'Hp': Hp, 'Wp': Wp}
+        groups = self._groups(B, mode)
         plan.add('pack_burst', lib.dbsr_pack_burst, B, N, H, W, bufs['burst'].data_ptr(), raw.d(0), Hp, Wp,
-                 rgb.d(0) if not zero_flow else L.NULL_TENSOR)
-        # Two lanes: the alignment chain (PWC-Net -> offsets -> offset-feature extractor, many small
-        # latency-bound launches) runs on a high-priority side stream beside the per-frame encoder
-        # (large launches); they meet at the warp.
-        plan.fork(1, dev, priority=-1)
-        # while the side lane runs, lane-0 persistent convs leave a quarter of the CUs to it
+                 rgb.d(0) if not self.zero_flow else L.NULL_TENSOR)
+        # lane-0 persistent convs issued while the side lane runs leave part of the CUs to it
         plan_cap = int(torch.cuda.get_device_properties(dev).multi_processor_count * DBSREngine.LANE0_CU_SHARE) \
             if Plan.MULTI_STREAM else 0
-        # ---------------- alignment (PWC-Net) ----------------
-        if not zero_flow:
-            flow_out = NHWC(P, Hp // 4, Wp // 4, 2, torch.float32, dev)
-            self.pwc.build(plan, dt, dev, F, Hp, Wp, P, first_map=(N - 1, N, 0, 0), second_map=(N - 1, N, 1, 1),
-                           rgb=rgb, flow_out=flow_out)
-            plan.add('flow_finalize', lib.dbsr_flow_finalize, B, N, Hp // 4, Wp // 4, flow_out.d(0), H, W, Hp, Wp,
-                     bufs['offsets'].data_ptr(), 1.0, om.d(0))
-            plan.keep.append(flow_out)
-        # (zero flow: offsets and om stay zero from initialisation)
-        pd = self.proj.cout
-        od = self.ofe_init.cout
-        WP = NHWC(F, H, W, 2 * pd + od, dt, dev)
-        # offset-feature extractor (merging.py:85-87) -> WP[..., 2*pd:]
-        o = [NHWC(F, H, W, od, dt, dev) for _ in range(3)]
-        plan.conv('merge.ofe.init', self.ofe_init, F, om, 0, hw, o[0], 0, L.ACT_RELU)
-        a = 0
-        for k, (c1, c2) in enumerate(self.ofe_res):
-            b, c = [j for j in range(3) if j != a]
-            last = k == len(self.ofe_res) - 1
-            plan.conv(f'merge.ofe.res{k}.conv1', c1, F, o[a], 0, hw, o[b], 0, L.ACT_RELU)
-            if last:
-                plan.conv(f'merge.ofe.res{k}.conv2', c2, F, o[b], 0, hw, WP, 2 * pd, L.ACT_NONE, res=o[a],
-                          post_act=L.ACT_RELU)
-            else:
-                plan.conv(f'merge.ofe.res{k}.conv2', c2, F, o[b], 0, hw, o[c], 0, L.ACT_NONE, res=o[a],
-                          post_act=L.ACT_RELU)
-                a = c
-        if not self.ofe_res:
-            raise NotImplementedError('num_offset_feat_extractor_res must be >= 1')
+        plan.fork(1, dev, priority=-1)
+        WPs = [self._emit_align(plan, groups[0], N, H, W, sh)]
         plan.switch(0)
         plan.max_blocks = plan_cap
-        # ---------------- encoder (encoders.py:66-72) ----------------
+        # ---------------- encoder (encoders.py:66-72), whole batch ----------------
         e = [NHWC(F, H, W, r8(self.enc_init.cout), dt, dev) for _ in range(3)]
         plan.conv('enc.init', self.enc_init, F, raw, 0, hw, e[0], 0, L.ACT_RELU)
         i = self._resblocks(plan, 'enc.res', self.enc_res, F, hw, e, 0, dt)
-        E = NHWC(F, H, W, C, dt, dev)
         plan.conv('enc.out', self.enc_out, F, e[i], 0, hw, E, 0, L.ACT_RELU)
-        # ---------------- merging (merging.py:61-127) ----------------
-        PJ = NHWC(F, H, W, r8(pd), dt, dev)
         plan.conv('merge.proj_ref', self.proj, B, E, 0, hw, PJ, 0, L.ACT_RELU, xmap=(1, N, 0, 1), ymap=(1, N, 0, 1))
-        plan.join(1)
-        plan.max_blocks = 0
-        # ---------------- warp (encoders.py:80) ----------------
-        Wf = NHWC(max(P, 1), H, W, C, dt, dev)
+        plan.keep.extend([raw, rgb, om, e, E, PJ])
+        FW = NHWC(F, H, W, C, dt, dev) if mode == 'full' else None
+        if mode == 'full':
+            bufs['pred'] = torch.zeros(B, 3, H * self.s, W * self.s, dtype=torch.float32, device=dev)
+        plan.fuse_ops = []
         es = 4 if dt == torch.float32 else 2
-        if P > 0:
-            plan.add('warp', lib.dbsr_warp_bilinear, P, H, W, C, E.d(0, (N - 1, N, 1, 1)), bufs['offsets'].data_ptr(),
-                     2 * H * W, Wf.d(0), work=('byte', 2.0 * P * C * H * W * es + 8.0 * P * H * W))
-        if P > 0:
-            plan.conv('merge.proj_oth', self.proj, P, Wf, 0, hw, PJ, 0, L.ACT_RELU, ymap=(N - 1, N, 1, 1))
-        plan.add('merge.prep', lib.dbsr_merge_prep, B, N, H * W, pd, PJ.d(0), WP.d(0))
-        q = [NHWC(F, H, W, self.wp_init.cout, dt, dev) for _ in range(3)]
-        plan.conv('merge.wp.init', self.wp_init, F, WP, 0, hw, q[0], 0, L.ACT_RELU)
-        i = self._resblocks(plan, 'merge.wp.res', self.wp_res, F, hw, q, 0, dt)
-        LG = NHWC(F, H, W, C, dt, dev)
-        plan.conv('merge.wp.out', self.wp_out, F, q[i], 0, hw, LG, 0, L.ACT_NONE)
-        plan.keep.extend([raw, rgb, om, e, E, Wf, PJ, WP, o, q, LG])
-        if mode == 'partial':
-            ST = torch.zeros(B, H, W, 3 * C, dtype=torch.float32, device=dev)
-            plan.add('merge.fuse_partial', lib.dbsr_fuse_partial, B, N, H * W, C, first_frame, LG.d(0),
-                     E.d(0, (1, N, 0, 1)), Wf.d(0), ST.data_ptr())
-            bufs['stats'] = ST
-            plan.finalize_workspace(dev)
-            plan.bufs = bufs
-            plan.shape = (B, N, H, W)
-            return plan
-        FUS = NHWC(B, H, W, C, dt, dev)
-        FW = NHWC(F, H, W, C, dt, dev)
-        bufs['fw_desc'] = FW.d(0)
-        fuse_args = [B, N, H * W, C, LG.d(0), E.d(0, (1, N, 0, 1)), Wf.d(0), FUS.d(0), FW.d(0)]
-        plan.add('merge.fuse', lib.dbsr_fuse_softmax, *fuse_args)
-        fuse_idx = len(plan.ops) - 1
-        plan.fuse_bytes = ((2.0 * N + 1) * B * C * H * W * es, 1.0 * N * B * C * H * W * es)
-        self._decoder(plan, B, H, W, FUS, bufs)
-        plan.keep.extend([FUS, FW])
+        for gi, grp in enumerate(groups):
+            plan.join(1)                      # lane 0 waits for this group's alignment chain
+            if gi + 1 < len(groups):
+                plan.switch(1)                # ... while lane 1 aligns the next group
+                WPs.append(self._emit_align(plan, groups[gi + 1], N, H, W, sh))
+                plan.switch(0)
+                plan.max_blocks = plan_cap
+            else:
+                plan.max_blocks = 0
+            LG, Wf = self._emit_merge(plan, grp, N, H, W, sh, WPs[gi])
+            g0, g1 = grp
+            Bg = g1 - g0
+            if mode == 'partial':
+                ST = torch.zeros(B, H, W, 3 * C, dtype=torch.float32, device=dev)
+                plan.add('merge.fuse_partial', lib.dbsr_fuse_partial, B, N, H * W, C, first_frame, LG.d(0),
+                         E.d(0, (1, N, 0, 1)), Wf.d(0), ST.data_ptr())
+                bufs['stats'] = ST
+                break
+            FUS = NHWC(Bg, H, W, C, dt, dev)
+            fmap = (1, 1, g0 * N, 0)
+            args = [Bg, N, H * W, C, LG.d(0), E.d(0, (1, N, g0 * N, 1)), Wf.d(0), FUS.d(0), FW.d(0, fmap)]
+            plan.add('merge.fuse', lib.dbsr_fuse_softmax, *args)
+            plan.fuse_ops.append((len(plan.ops) - 1, args, FW.d(0, fmap),
+                                  ((2.0 * N + 1) * Bg * C * H * W * es, 1.0 * N * Bg * C * H * W * es)))
+            self._decoder(plan, Bg, H, W, FUS, bufs, pred_out=bufs['pred'][g0:g1])
+            plan.keep.append(FUS)
+        plan.max_blocks = 0
+        plan.keep.append(FW)
         plan.finalize_workspace(dev)
         plan.bufs = bufs
         plan.FW = FW
-        plan.fuse_idx = fuse_idx
-        plan.fuse_args = fuse_args
         plan.shape = (B, N, H, W)
         return plan
 
-    def _decoder(self, plan, B, H, W, FUS, bufs):
-        """ResPixShuffleConv (decoders.py:54-62) on the fused embedding FUS [B,H,W,C] -> bufs['pred']."""
+    def _decoder(self, plan, B, H, W, FUS, bufs, pred_out=None):
+        """ResPixShuffleConv (decoders.py:54-62) on the fused embedding FUS [B,H,W,C] -> pred_out (a [B,3,sH,sW]
+        fp32 view; default: a new bufs['pred'])."""
         dt, dev = self.dtype, self.device
         lib = L.lib()
         hw = (H, W)
@@ -586,8 +636,9 @@ class DBSREngine:
             plan.keep.append(kbuf)
             plan.add('dec.blur', lib.dbsr_gauss_blur3, B, H * S, W * S, pc, sh[0].d(0), kbuf, sh[1].d(0))
             a = 1
-        bufs['pred'] = torch.zeros(B, 3, H * S, W * S, dtype=torch.float32, device=dev)
-        pdesc = L.tensor_desc(bufs['pred'], 1, 0, img_stride=3 * H * S * W * S, dtype=torch.float32)
+        if pred_out is None:
+            pred_out = bufs['pred'] = torch.zeros(B, 3, H * S, W * S, dtype=torch.float32, device=dev)
+        pdesc = L.tensor_desc(pred_out, 1, 0, img_stride=3 * H * S * W * S, dtype=torch.float32)
         # bf16: the last post ResBlock's conv2 and the RGB predictor in one kernel (its 32-channel output
         # never reaches HBM; the head runs fp32 on the fp32 ResBlock output, decoders.py:59-61)
         head = None
@@ -611,11 +662,12 @@ class DBSREngine:
         return g
 
     def _set_fw(self, plan, want):
-        fn, args, name, lane = plan.ops[plan.fuse_idx]
-        args = list(plan.fuse_args)
-        args[-1] = plan.bufs['fw_desc'] if want else L.NULL_TENSOR
-        plan.ops[plan.fuse_idx] = (fn, tuple(args), name, lane)
-        plan.work[plan.fuse_idx] = ('byte', plan.fuse_bytes[0] + (plan.fuse_bytes[1] if want else 0.0))
+        for idx, args, fw_desc, (bytes_base, bytes_fw) in plan.fuse_ops:
+            fn, _, name, lane = plan.ops[idx]
+            a = list(args)
+            a[-1] = fw_desc if want else L.NULL_TENSOR
+            plan.ops[idx] = (fn, tuple(a), name, lane)
+            plan.work[idx] = ('byte', bytes_base + (bytes_fw if want else 0.0))
 
     def forward(self, burst):
         if not burst.is_cuda:
