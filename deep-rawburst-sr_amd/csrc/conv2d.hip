@@ -1346,13 +1346,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ws_kernel(ConvK k, int tiles_x
         for (int step = 0; step < C::STEPS; ++step) {
             // vector-memory work of this step: the next tile's halo (first half) and residual (second half;
             // its buffer was last read by the epilogue before this tile's barrier)
-#ifndef DBSR_WS_NODMA
             if (more) {
 #pragma unroll
                 for (int it = 0; it < C::PER; ++it)
                     if ((it * C::DMA_STEPS) / C::PER == step) dma(it, nxt, nbuf);
             }
-#endif
             if constexpr (RES_BUFS > 0) {
                 if (has_res && more) {
 #pragma unroll
