@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get('DBSR_HIP_LIB', os.path.join(_HERE, 'libdbsr_hip.so'))
 DBSR_F32, DBSR_BF16, DBSR_F16 = 0, 1, 2
 ACT_NONE, ACT_RELU, ACT_LRELU = 0, 1, 2
 OUT_NHWC, OUT_SHUFFLE, OUT_NCHW_F32 = 0, 1, 2
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 
 class FrameMap(ctypes.Structure):
@@ -85,6 +85,9 @@ def lib():
             'dbsr_warp_bilinear': ([c_int, c_int, c_int, c_int, Tensor, c_void_p, c_ll, Tensor, c_void_p], c_int),
             'dbsr_fuse_softmax': ([c_int, c_int, c_int, c_int, Tensor, Tensor, Tensor, Tensor, Tensor, c_void_p],
                                   c_int),
+            'dbsr_conv_fuse_softmax': ([ctypes.POINTER(ConvDesc), c_int, c_int, Tensor, Tensor, Tensor, Tensor,
+                                        c_void_p], c_int),
+            'dbsr_conv_fuse_ok': ([ctypes.POINTER(ConvDesc), c_int, c_int], c_int),
             'dbsr_fuse_partial': ([c_int, c_int, c_int, c_int, c_int, Tensor, Tensor, Tensor, c_void_p, c_void_p], c_int),
             'dbsr_fuse_combine': ([c_int, c_int, c_int, c_int, c_void_p, Tensor, c_void_p], c_int),
             'dbsr_conv_transpose_k4s2': ([c_int, c_int, c_int, c_int, c_int, Tensor, c_void_p, c_void_p, Tensor,
@@ -136,7 +139,7 @@ EXPORTED = ['dbsr_abi_version', 'dbsr_last_error', 'dbsr_conv_packed_elems', 'db
             'dbsr_set_conv_algo', 'dbsr_conv_kernel_for', 'dbsr_conv_workspace_bytes', 'dbsr_conv2d_head',
             'dbsr_conv_head_ok',
             'dbsr_correlation', 'dbsr_correlation_backward', 'dbsr_backwarp', 'dbsr_warp_bilinear', 'dbsr_fuse_softmax',
-            'dbsr_fuse_partial', 'dbsr_fuse_combine',
+            'dbsr_fuse_partial', 'dbsr_fuse_combine', 'dbsr_conv_fuse_softmax', 'dbsr_conv_fuse_ok',
             'dbsr_conv_transpose_k4s2', 'dbsr_pack_burst', 'dbsr_flow_finalize', 'dbsr_gauss_blur3',
             'dbsr_merge_prep', 'dbsr_pwc_assemble', 'dbsr_zero', 'dbsr_conv_wgrad_workspace_bytes', 'dbsr_conv_wgrad',
             'dbsr_chan_sum_workspace_bytes', 'dbsr_chan_sum', 'dbsr_l1_loss_backward', 'dbsr_unshuffle_gate',

@@ -26,6 +26,7 @@ Layout map (reference file:line per stage):
 import ctypes
 import math
 import os
+import types
 
 import torch
 
@@ -162,6 +163,42 @@ class Plan:
         it (dbsr_conv_head_ok), the conv's own output is not stored and the 1x1 head + ReLU writes out_desc
         (fp32 NCHW); the returned desc then has .fused_head = True.  gate: output *= (gate > 0) (training
         dgrad: the ReLU backward of the layer that produced the forward conv's input)."""
+        d = self._desc(name, pc, n_frames, x, xc0, in_hw, y, yc0, act, xmap, ymap, res, rc0, rmap, post_act,
+                       out_mode, shuffle, y_desc, cin, precise, gate, gc0, gmap)
+        self.convs.append((d, self.lane))
+        oh, ow = d.out_h, d.out_w
+        flop = 2.0 * n_frames * oh * ow * pc.cout * d.cin * pc.kh * pc.kw
+        d.fused_head = bool(head is not None and L.lib().dbsr_conv_head_ok(ctypes.byref(d)))
+        if d.fused_head:
+            hname, hw, hb, hdesc = head
+            self.keep.extend([hw, hb, hdesc])
+            flop += 2.0 * n_frames * oh * ow * hw.shape[0] * hw.shape[1]
+            self.add(name + '+' + hname, L.lib().dbsr_conv2d_head, ctypes.byref(d), hw.data_ptr(),
+                     hb.data_ptr() if hb is not None else None, hw.shape[0], hdesc, work=('flop', flop))
+            self.kernel[len(self.ops) - 1] = 'conv3x3_pipe'
+            return d
+        self.add(name, L.lib().dbsr_conv2d, ctypes.byref(d), work=('flop', flop))
+        self.kernel[len(self.ops) - 1] = {4: 'conv3x3_ws', 2: 'conv3x3_pipe', 1: 'conv3x3_tiled', 3: 'conv1x1_shuffle'}.get(L.lib().dbsr_conv_kernel_for(d),
+                                                                                      'conv2d_generic')
+        return d
+
+    def conv_fuse(self, name, pc, B, N, x, in_hw, ref, oth, fused, weights):
+        """The weight predictor's last conv + softmax over the burst + fusion in one launch
+        (dbsr_conv_fuse_softmax: the logits never reach memory).  Returns the op index, or None when the
+        library does not serve the shape (the caller then emits the conv and dbsr_fuse_softmax)."""
+        d = self._desc(name, pc, B * N, x, 0, in_hw, None, 0, L.ACT_NONE, IDENTITY, IDENTITY, None, 0, IDENTITY,
+                       L.ACT_NONE, L.OUT_NHWC, 0, L.NULL_TENSOR, None, False, None, 0, IDENTITY)
+        if not L.lib().dbsr_conv_fuse_ok(ctypes.byref(d), B, N):
+            return None
+        H, W = in_hw
+        flop = 2.0 * B * N * H * W * pc.cout * d.cin * pc.kh * pc.kw
+        self.add(name, L.lib().dbsr_conv_fuse_softmax, ctypes.byref(d), B, N, ref, oth, fused, weights,
+                 work=('flop', flop))
+        self.kernel[len(self.ops) - 1] = 'conv_fuse'
+        return len(self.ops) - 1
+
+    def _desc(self, name, pc, n_frames, x, xc0, in_hw, y, yc0, act, xmap, ymap, res, rc0, rmap, post_act, out_mode,
+              shuffle, y_desc, cin, precise, gate, gc0, gmap):
         oh, ow = pc.out_hw(*in_hw)
         assert cin is None or cin == pc.cin, (name, cin, pc.cin)
         d = L.ConvDesc()
@@ -183,20 +220,6 @@ class Plan:
         d.precise = 1 if precise else 0
         d.max_blocks = self.max_blocks if self.lane == 0 else 0
         self.keep.append(d)
-        self.convs.append((d, self.lane))
-        flop = 2.0 * n_frames * oh * ow * pc.cout * d.cin * pc.kh * pc.kw
-        d.fused_head = bool(head is not None and L.lib().dbsr_conv_head_ok(ctypes.byref(d)))
-        if d.fused_head:
-            hname, hw, hb, hdesc = head
-            self.keep.extend([hw, hb, hdesc])
-            flop += 2.0 * n_frames * oh * ow * hw.shape[0] * hw.shape[1]
-            self.add(name + '+' + hname, L.lib().dbsr_conv2d_head, ctypes.byref(d), hw.data_ptr(),
-                     hb.data_ptr() if hb is not None else None, hw.shape[0], hdesc, work=('flop', flop))
-            self.kernel[len(self.ops) - 1] = 'conv3x3_pipe'
-            return d
-        self.add(name, L.lib().dbsr_conv2d, ctypes.byref(d), work=('flop', flop))
-        self.kernel[len(self.ops) - 1] = {4: 'conv3x3_ws', 2: 'conv3x3_pipe', 1: 'conv3x3_tiled', 3: 'conv1x1_shuffle'}.get(L.lib().dbsr_conv_kernel_for(d),
-                                                                                      'conv2d_generic')
         return d
 
     def finalize_workspace(self, device):
@@ -394,6 +417,12 @@ class DBSREngine:
                               # half-batch chains take twice as long (tools/sweep_engine.py)
     # bf16: fuse the RGB predictor into the last decoder ResBlock conv (False: separate fp32 kernel)
     FUSED_HEAD = True
+    # weight-predictor input conv split into a per-frame [proj, offfeat] conv + a per-burst base conv
+    LINEAR_SPLIT = True
+    # weight-predictor output conv + softmax + fusion in one kernel (dbsr_conv_fuse_softmax: the logits never
+    # reach memory).  Off: measured 468-563 us per cfg2 step against 407 us for dbsr_conv2d (pipelined) +
+    # dbsr_fuse_softmax -- one wave per SIMD exposes the per-frame epilogue and latencies
+    FUSED_WP_OUT = False
 
     def __init__(self, net):
         self.net = net
@@ -423,6 +452,19 @@ class DBSREngine:
         self.ofe_res = [(W.conv(b.conv1[0]), W.conv(b.conv2[0])) for b in ofe[1:]]
         wp = list(mer.weight_predictor)
         self.wp_init = W.conv(wp[0][0])
+        # linearity split of the first weight-predictor conv (merging.py:87-113): its input is
+        # [base, proj_f - base, offfeat_f] with base = proj of the burst's reference frame (use_base_frame), so
+        # conv(W)(input) = conv([W_diff | W_off])([proj_f, offfeat_f]) + conv(W_base - W_diff)(base): the second
+        # term is one conv per burst instead of per frame, and the merge-prep copy of base / diff disappears
+        pd = mer.feat_project_layer[0].out_channels
+        self.wp_split = None
+        if DBSREngine.LINEAR_SPLIT and getattr(mer, 'use_base_frame', False) and pd % 32 == 0:
+            w0 = wp[0][0].weight.detach().float()
+            rest = types.SimpleNamespace(weight=w0[:, pd:].contiguous(), bias=wp[0][0].bias, stride=(1,),
+                                         padding=wp[0][0].padding, dilation=wp[0][0].dilation)
+            base = types.SimpleNamespace(weight=(w0[:, :pd] - w0[:, pd:2 * pd]).contiguous(), bias=None,
+                                         stride=(1,), padding=wp[0][0].padding, dilation=wp[0][0].dilation)
+            self.wp_split = (W.conv(rest), W.conv(base))
         self.wp_res = [(W.conv(b.conv1[0]), W.conv(b.conv2[0])) for b in wp[1:-1]]
         self.wp_out = W.conv(wp[-1][0])
         self.dec_init = W.conv(dec.init_layer[0])
@@ -487,7 +529,9 @@ class DBSREngine:
             plan.keep.append(flow_out)
         # (zero flow: offsets and om stay zero from initialisation)
         pd, od = self.proj.cout, self.ofe_init.cout
-        WP = NHWC(Fg, H, W, 2 * pd + od, dt, dev)
+        # weight-predictor input: [base, diff, offfeat] (merging.py:110), or [proj, offfeat] with the split
+        oc = pd if self.wp_split is not None else 2 * pd
+        WP = NHWC(Fg, H, W, oc + od, dt, dev)
         o = [NHWC(Fg, H, W, od, dt, dev) for _ in range(3)]
         plan.conv('merge.ofe.init', self.ofe_init, Fg, sh['om'], 0, hw, o[0], 0, L.ACT_RELU, xmap=fmap)
         a = 0
@@ -498,7 +542,7 @@ class DBSREngine:
             last = k == len(self.ofe_res) - 1
             plan.conv(f'merge.ofe.res{k}.conv1', c1, Fg, o[a], 0, hw, o[b], 0, L.ACT_RELU)
             if last:
-                plan.conv(f'merge.ofe.res{k}.conv2', c2, Fg, o[b], 0, hw, WP, 2 * pd, L.ACT_NONE, res=o[a],
+                plan.conv(f'merge.ofe.res{k}.conv2', c2, Fg, o[b], 0, hw, WP, oc, L.ACT_NONE, res=o[a],
                           post_act=L.ACT_RELU)
             else:
                 plan.conv(f'merge.ofe.res{k}.conv2', c2, Fg, o[b], 0, hw, o[c], 0, L.ACT_NONE, res=o[a],
@@ -524,15 +568,36 @@ class DBSREngine:
             plan.add('warp', lib.dbsr_warp_bilinear, Pg, H, W, C, E.d(0, (N - 1, N, 1 + off_f, 1)),
                      sh['offsets'][off_p:].data_ptr(), 2 * H * W, Wf.d(0),
                      work=('byte', 2.0 * Pg * C * H * W * es + 8.0 * Pg * H * W))
-            plan.conv('merge.proj_oth', self.proj, Pg, Wf, 0, hw, PJ, 0, L.ACT_RELU, ymap=(N - 1, N, 1 + off_f, 1))
-        plan.add('merge.prep', lib.dbsr_merge_prep, Bg, N, H * W, pd, PJ.d(0, (1, 1, off_f, 0)), WP.d(0))
         q = [NHWC(Fg, H, W, self.wp_init.cout, dt, dev) for _ in range(3)]
-        plan.conv('merge.wp.init', self.wp_init, Fg, WP, 0, hw, q[0], 0, L.ACT_RELU)
+        if self.wp_split is not None:
+            # projections straight into WP[..., :pd]; the base term once per burst, added (broadcast over the
+            # burst's frames) as the residual of the per-frame conv before its ReLU
+            rest, basec = self.wp_split
+            plan.conv('merge.proj_ref', self.proj, Bg, E, 0, hw, WP, 0, L.ACT_RELU, xmap=(1, N, off_f, 1),
+                      ymap=(1, N, 0, 1))
+            if Pg > 0:
+                plan.conv('merge.proj_oth', self.proj, Pg, Wf, 0, hw, WP, 0, L.ACT_RELU, ymap=(N - 1, N, 1, 1))
+            BS = NHWC(Bg, H, W, r8(basec.cout), dt, dev)
+            plan.conv('merge.wp.base', basec, Bg, WP, 0, hw, BS, 0, L.ACT_NONE, xmap=(1, N, 0, 1))
+            plan.conv('merge.wp.init', rest, Fg, WP, 0, hw, q[0], 0, L.ACT_NONE, res=BS, rmap=(N, 1, 0, 0),
+                      post_act=L.ACT_RELU)
+            plan.keep.append(BS)
+        else:
+            if Pg > 0:
+                plan.conv('merge.proj_oth', self.proj, Pg, Wf, 0, hw, PJ, 0, L.ACT_RELU,
+                          ymap=(N - 1, N, 1 + off_f, 1))
+            plan.add('merge.prep', lib.dbsr_merge_prep, Bg, N, H * W, pd, PJ.d(0, (1, 1, off_f, 0)), WP.d(0))
+            plan.conv('merge.wp.init', self.wp_init, Fg, WP, 0, hw, q[0], 0, L.ACT_RELU)
         i = self._resblocks(plan, 'merge.wp.res', self.wp_res, Fg, hw, q, 0, dt)
-        LG = NHWC(Fg, H, W, C, dt, dev)
-        plan.conv('merge.wp.out', self.wp_out, Fg, q[i], 0, hw, LG, 0, L.ACT_NONE)
-        plan.keep.extend([Wf, q, LG])
-        return LG, Wf
+        plan.keep.extend([Wf, q])
+        return q[i], Wf
+
+    def _emit_logits(self, plan, Fg, H, W, h):
+        """The weight predictor's last conv (merging.py:55-57) into a logits buffer LG [Fg,H,W,C]."""
+        LG = NHWC(Fg, H, W, self.enc_out.cout, self.dtype, self.device)
+        plan.conv('merge.wp.out', self.wp_out, Fg, h, 0, (H, W), LG, 0, L.ACT_NONE)
+        plan.keep.append(LG)
+        return LG
 
     def _build(self, B, N, H, W, mode='full', first_frame=0):
         """mode 'full': the whole forward.  mode 'partial' (frame-sharded fusion): stop after
@@ -557,7 +622,7 @@ class DBSREngine:
         bufs['offsets'] = torch.zeros(P, 2, H, W, dtype=torch.float32, device=dev)
         om = NHWC(F, H, W, 8, dt, dev)
         E = NHWC(F, H, W, C, dt, dev)
-        PJ = NHWC(F, H, W, r8(self.proj.cout), dt, dev)
+        PJ = NHWC(F, H, W, r8(self.proj.cout), dt, dev) if self.wp_split is None else None
         sh = {'rgb': rgb, 'offsets': bufs['offsets'], 'om': om, 'E': E, 'PJ': PJ, 'Hp': Hp, 'Wp': Wp}
         groups = self._groups(B, mode)
         plan.add('pack_burst', lib.dbsr_pack_burst, B, N, H, W, bufs['burst'].data_ptr(), raw.d(0), Hp, Wp,
@@ -574,7 +639,9 @@ class DBSREngine:
         plan.conv('enc.init', self.enc_init, F, raw, 0, hw, e[0], 0, L.ACT_RELU)
         i = self._resblocks(plan, 'enc.res', self.enc_res, F, hw, e, 0, dt)
         plan.conv('enc.out', self.enc_out, F, e[i], 0, hw, E, 0, L.ACT_RELU)
-        plan.conv('merge.proj_ref', self.proj, B, E, 0, hw, PJ, 0, L.ACT_RELU, xmap=(1, N, 0, 1), ymap=(1, N, 0, 1))
+        if self.wp_split is None:
+            plan.conv('merge.proj_ref', self.proj, B, E, 0, hw, PJ, 0, L.ACT_RELU, xmap=(1, N, 0, 1),
+                      ymap=(1, N, 0, 1))
         plan.keep.extend([raw, rgb, om, e, E, PJ])
         FW = NHWC(F, H, W, C, dt, dev) if mode == 'full' else None
         if mode == 'full':
@@ -590,10 +657,11 @@ class DBSREngine:
                 plan.max_blocks = plan_cap
             else:
                 plan.max_blocks = 0
-            LG, Wf = self._emit_merge(plan, grp, N, H, W, sh, WPs[gi])
+            h, Wf = self._emit_merge(plan, grp, N, H, W, sh, WPs[gi])
             g0, g1 = grp
             Bg = g1 - g0
             if mode == 'partial':
+                LG = self._emit_logits(plan, Bg * N, H, W, h)
                 ST = torch.zeros(B, H, W, 3 * C, dtype=torch.float32, device=dev)
                 plan.add('merge.fuse_partial', lib.dbsr_fuse_partial, B, N, H * W, C, first_frame, LG.d(0),
                          E.d(0, (1, N, 0, 1)), Wf.d(0), ST.data_ptr())
@@ -601,10 +669,17 @@ class DBSREngine:
                 break
             FUS = NHWC(Bg, H, W, C, dt, dev)
             fmap = (1, 1, g0 * N, 0)
-            args = [Bg, N, H * W, C, LG.d(0), E.d(0, (1, N, g0 * N, 1)), Wf.d(0), FUS.d(0), FW.d(0, fmap)]
-            plan.add('merge.fuse', lib.dbsr_fuse_softmax, *args)
-            plan.fuse_ops.append((len(plan.ops) - 1, args, FW.d(0, fmap),
-                                  ((2.0 * N + 1) * Bg * C * H * W * es, 1.0 * N * Bg * C * H * W * es)))
+            feats = [E.d(0, (1, N, g0 * N, 1)), Wf.d(0), FUS.d(0), FW.d(0, fmap)]
+            idx = plan.conv_fuse('merge.wp.out+fuse', self.wp_out, Bg, N, h, hw, *feats) \
+                if DBSREngine.FUSED_WP_OUT else None
+            if idx is not None:
+                plan.fuse_ops.append((idx, plan.ops[idx][1], FW.d(0, fmap), None))
+            else:
+                LG = self._emit_logits(plan, Bg * N, H, W, h)
+                args = [Bg, N, H * W, C, LG.d(0)] + feats
+                plan.add('merge.fuse', lib.dbsr_fuse_softmax, *args)
+                plan.fuse_ops.append((len(plan.ops) - 1, args, FW.d(0, fmap),
+                                      ((2.0 * N + 1) * Bg * C * H * W * es, 1.0 * N * Bg * C * H * W * es)))
             self._decoder(plan, Bg, H, W, FUS, bufs, pred_out=bufs['pred'][g0:g1])
             plan.keep.append(FUS)
         plan.max_blocks = 0
@@ -662,12 +737,13 @@ class DBSREngine:
         return g
 
     def _set_fw(self, plan, want):
-        for idx, args, fw_desc, (bytes_base, bytes_fw) in plan.fuse_ops:
+        for idx, args, fw_desc, nbytes in plan.fuse_ops:
             fn, _, name, lane = plan.ops[idx]
             a = list(args)
             a[-1] = fw_desc if want else L.NULL_TENSOR
             plan.ops[idx] = (fn, tuple(a), name, lane)
-            plan.work[idx] = ('byte', bytes_base + (bytes_fw if want else 0.0))
+            if nbytes is not None:            # (the fused conv's work stays its FLOPs)
+                plan.work[idx] = ('byte', nbytes[0] + (nbytes[1] if want else 0.0))
 
     def forward(self, burst):
         if not burst.is_cuda:

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DBSR_ABI_VERSION 9
+#define DBSR_ABI_VERSION 10
 
 enum { DBSR_F32 = 0, DBSR_BF16 = 1, DBSR_F16 = 2 };
 enum { DBSR_ACT_NONE = 0, DBSR_ACT_RELU = 1, DBSR_ACT_LRELU = 2 };      /* LeakyReLU slope 0.1 */
@@ -153,6 +153,17 @@ int dbsr_warp_bilinear(int n, int h, int w, int c, dbsr_tensor feat, const float
  * weights (optional, ptr NULL to skip): NHWC images b*N+n.  fused: NHWC images b. */
 int dbsr_fuse_softmax(int B, int N, int hw, int c, dbsr_tensor logits, dbsr_tensor ref, dbsr_tensor oth,
                       dbsr_tensor fused, dbsr_tensor weights, void* stream);
+
+/* The weight predictor's last conv fused with the softmax over the burst and the weighted sum
+ * (models/dbsr/merging.py:55-57,113-124): logits = conv(d) for the B*N frames of
+ * d->x (frame b*N+n of burst b) never reach memory -- each (burst, 16x4 tile, 64 channels) block keeps
+ * all N frames' logits (rounded to the conv dtype, as dbsr_conv2d would store them) in registers.
+ * ref / oth / fused / weights address as in dbsr_fuse_softmax (c = d->cout); d->y, d->res are unused.
+ * Requires dbsr_conv_fuse_ok(d, B, N): 16-bit 3x3/s1/p1/d1, cin_pad 64 or 128, cout % 64 == 0,
+ * d->n_frames == B*N, N == 14, width % 16 == 0, height % 4 == 0. */
+int dbsr_conv_fuse_softmax(const dbsr_conv_desc* d, int B, int N, dbsr_tensor ref, dbsr_tensor oth,
+                           dbsr_tensor fused, dbsr_tensor weights, void* stream);
+int dbsr_conv_fuse_ok(const dbsr_conv_desc* d, int B, int N);
 
 /* Frame-sharded fusion (the softmax over the burst of models/dbsr/merging.py:116-124
  * split over ranks holding disjoint frame subsets).  dbsr_fuse_partial: statistics of the local frames

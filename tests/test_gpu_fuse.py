@@ -1,0 +1,147 @@
+"""dbsr_conv_fuse_softmax (the weight predictor's last conv + softmax over the
+burst + fusion in one kernel, models/dbsr/merging.py:55-57,113-124) against torch on the same 16-bit
+operands, and against the two-kernel path (dbsr_conv2d to a logits buffer + dbsr_fuse_softmax).
+
+Tolerances: the logits are rounded to the compute dtype as the two-kernel path stores them, but their
+K sum runs in two halves (the kernel's waves split K) and the softmax statistics accumulate online, so
+against the two-kernel path >= 99 % of weights / fused values agree to 1 ulp of the output dtype and
+all within the torch tolerance below.
+Against torch (fp32 conv of the rounded operands, fp32 softmax): weights atol 2e-3 + rtol 5e-2, fused
+atol 2e-2 (a logit that lands on the other side of a 16-bit rounding boundary moves its weight)."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+def _case(B, N, H, W, cin, C, dt, seed, want_fw=True):
+    from dbsr_amd import _lib as L
+    from dbsr_amd.engine import NHWC, PackedConv, Plan
+    gen = torch.Generator().manual_seed(seed)
+    h = torch.randn(B * N, cin, H, W, generator=gen)
+    conv = torch.nn.Conv2d(cin, C, 3, padding=1)
+    with torch.no_grad():
+        conv.weight.copy_(torch.randn(C, cin, 3, 3, generator=gen) * (3.0 / (cin * 9) ** 0.5))
+        conv.bias.copy_(torch.randn(C, generator=gen))
+    feat = torch.randn(B, N, C, H, W, generator=gen)
+    w_cpu, b_cpu = conv.weight.detach().clone(), conv.bias.detach().clone()
+    dev = torch.device(DEV)
+    s = torch.cuda.current_stream().cuda_stream
+    pc = PackedConv(conv.to(dev), dt, dev, s)
+    X = NHWC(B * N, H, W, cin, dt, dev)
+    X.t.copy_(h.permute(0, 2, 3, 1).to(dt))
+    E = NHWC(B * N, H, W, C, dt, dev)           # frame embeddings, ref = frame b*N
+    E.t.copy_(feat.reshape(B * N, C, H, W).permute(0, 2, 3, 1).to(dt))
+    P = B * (N - 1)
+    Wf = NHWC(P, H, W, C, dt, dev)              # "warped" frames 1..N-1 of each burst
+    Wf.t.copy_(feat[:, 1:].reshape(P, C, H, W).permute(0, 2, 3, 1).to(dt))
+    outs = {}
+    for fused_path in (True, False):
+        FUS = NHWC(B, H, W, C, dt, dev)
+        FW = NHWC(B * N, H, W, C, dt, dev)
+        plan = Plan()
+        feats = [E.d(0, (1, N, 0, 1)), Wf.d(0), FUS.d(0), FW.d(0) if want_fw else L.NULL_TENSOR]
+        if fused_path:
+            idx = plan.conv_fuse('fz', pc, B, N, X, (H, W), *feats)
+            assert idx is not None, 'dbsr_conv_fuse_ok rejected the case'
+        else:
+            LG = NHWC(B * N, H, W, C, dt, dev)
+            plan.conv('lg', pc, B * N, X, 0, (H, W), LG, 0, L.ACT_NONE)
+            plan.add('fuse', L.lib().dbsr_fuse_softmax, B, N, H * W, C, LG.d(0), *feats)
+        plan.finalize_workspace(dev)
+        plan.run(s)
+        torch.cuda.synchronize()
+        outs[fused_path] = (FUS.t.float().cpu(), FW.t.float().cpu())
+    # torch reference on the rounded operands; logits rounded like the stored ones
+    hb = h.to(dt).float()
+    wb = w_cpu.to(dt).float()
+    lg = F.conv2d(hb, wb, b_cpu, padding=1).to(dt).float().reshape(B, N, C, H, W)
+    wts = torch.softmax(lg, dim=1)
+    fz = (feat.to(dt).float() * wts).sum(dim=1)
+    ref = (fz.permute(0, 2, 3, 1), wts.reshape(B * N, C, H, W).permute(0, 2, 3, 1))
+    return outs, ref
+
+
+def _ulp_close(a, b, dt, atol=2e-3):
+    """<= 1 ulp of the output dtype (bf16 <= 2^-7, fp16 <= 2^-10 relative) on >= 99 % of the values;
+    the rest within the torch tolerance (a logit summed in another order can round to the neighbouring
+    16-bit value, which moves its weight by up to |l| * ulp)."""
+    eps = 2.0 ** -7 if dt == torch.bfloat16 else 2.0 ** -10
+    bad = (a - b).abs() > eps * torch.maximum(a.abs(), b.abs()) + 1e-6
+    frac = bad.float().mean().item()
+    assert frac <= 1e-2, '%d of %d beyond 1 ulp' % (int(bad.sum()), bad.numel())
+    np.testing.assert_allclose(a.numpy(), b.numpy(), atol=atol, rtol=5e-2)
+
+
+@pytest.mark.parametrize('case', [(2, 14, 48, 48, 128, 512, torch.bfloat16),    # the bench shape's layer
+                                  (1, 14, 32, 16, 128, 128, torch.float16),     # fp16, non-square
+                                  (3, 14, 8, 48, 128, 192, torch.bfloat16)])    # 3 channel slices
+def test_conv_fuse_vs_two_kernel_and_torch(case):
+    B, N, H, W, cin, C, dt = case
+    outs, (rf, rw) = _case(B, N, H, W, cin, C, dt, seed=B * 100 + H + C)
+    (f1, w1), (f0, w0) = outs[True], outs[False]
+    _ulp_close(w1, w0, dt)
+    _ulp_close(f1, f0, dt, atol=2e-2)
+    # a logit l rounded to the other side of a 16-bit boundary than torch's moves its weight by up to
+    # |l| * 2^-8 (bf16) relative: rtol 5e-2 at the |l| <~ 6 of these cases
+    np.testing.assert_allclose(w1.numpy(), rw.numpy(), atol=2e-3, rtol=5e-2)
+    np.testing.assert_allclose(f1.numpy(), rf.numpy(), atol=2e-2, rtol=1e-2)
+    # the weights of a pixel sum to 1 over the burst
+    s = w1.reshape(B, N, H, W, C).sum(dim=1)
+    assert (s - 1).abs().max() < 0.05
+
+
+def test_conv_fuse_without_aux_weights():
+    outs, (rf, _) = _case(1, 14, 16, 48, 128, 64, torch.bfloat16, seed=7, want_fw=False)
+    f1, w1 = outs[True]
+    assert w1.abs().max() == 0                   # aux output skipped
+    np.testing.assert_allclose(f1.numpy(), rf.numpy(), atol=2e-2, rtol=1e-2)
+
+
+def test_conv_fuse_rejects_unsupported():
+    from dbsr_amd import _lib as L
+    d = L.ConvDesc()
+    d.n_frames = 13 * 2
+    d.x = L.Tensor(1, L.DBSR_BF16, 48 * 48 * 128, 128, 0, L.FrameMap(1, 1, 0, 1))
+    d.in_h = d.in_w = d.out_h = d.out_w = 48
+    d.cin, d.cout, d.kh, d.kw, d.stride, d.pad, d.dil = 128, 512, 3, 3, 1, 1, 1
+    d.w = 1
+    assert L.lib().dbsr_conv_fuse_ok(ctypes.byref(d), 2, 13) == 0          # burst size 13
+    d.n_frames = 28
+    assert L.lib().dbsr_conv_fuse_ok(ctypes.byref(d), 2, 14) == 1
+    d.x.dtype = L.DBSR_F32
+    assert L.lib().dbsr_conv_fuse_ok(ctypes.byref(d), 2, 14) == 0          # fp32: two-kernel path
+
+
+def test_engine_fused_wp_out_matches_default(synth_sd):
+    """The whole bf16 forward with DBSREngine.FUSED_WP_OUT on (weight-predictor output conv + softmax +
+    fusion in one launch) against the default two-kernel plan, B=2 N=14 48x48: pred within 2^-6 and the
+    fusion weights within the torch tolerance above."""
+    import dbsr_amd
+    from dbsr_amd.burst import synthetic_bursts
+    from dbsr_amd.engine import DBSREngine
+    burst, _ = synthetic_bursts(2, 14, 48, 48, sr_factor=8, seed=77)
+    burst = burst.to(DEV)
+    outs = {}
+    old = DBSREngine.FUSED_WP_OUT
+    try:
+        for flag in (True, False):
+            DBSREngine.FUSED_WP_OUT = flag
+            net = dbsr_amd.dbsrnet_cvpr2021(**dbsr_amd.DBSR_SYNTHETIC_KWARGS)
+            net.load_state_dict(synth_sd)
+            net = net.to(DEV).eval().set_compute_dtype(torch.bfloat16)
+            with torch.no_grad():
+                pred, aux = net(burst)
+            names = [name for _, _, name, _ in net._engine.plans[(2, 14, 48, 48)].ops]
+            assert ('merge.wp.out+fuse' in names) == flag, names
+            outs[flag] = (pred.float().cpu(), aux['fusion_weights'].float().cpu())
+    finally:
+        DBSREngine.FUSED_WP_OUT = old
+    (p1, w1), (p0, w0) = outs[True], outs[False]
+    assert (p1 - p0).abs().max() < 2 ** -6
+    np.testing.assert_allclose(w1.numpy(), w0.numpy(), atol=2e-3, rtol=5e-2)
