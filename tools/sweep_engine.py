@@ -1,6 +1,6 @@
 """A/B the engine's scheduling knobs on the bench workload.
-Usage: python tools/sweep_engine.py 'LANE0_CU_SHARE=0.5,PIPELINE_GROUPS=1' 'PIPELINE_GROUPS=2' ...
-Each argument is one configuration of DBSREngine class attributes; prints bursts/s per configuration."""
+Usage: python tools/sweep_engine.py 'LANE0_CU_SHARE=0.5,PIPELINE_GROUPS=1' 'PIPELINE_GROUPS=2' 'Plan.INTERLEAVE_LANES=0' ...
+Each argument is one configuration of DBSREngine (or Plan.*) class attributes; prints bursts/s per configuration."""
 import json
 import os
 import subprocess
@@ -16,7 +16,9 @@ import dbsr_amd.engine as e
 for kv in %r.split(','):
     if kv:
         k, v = kv.split('=')
-        setattr(e.DBSREngine, k, type(getattr(e.DBSREngine, k))(float(v)) if '.' in v else int(v))
+        cls = e.Plan if k.startswith('Plan.') else e.DBSREngine
+        k = k.split('.')[-1]
+        setattr(cls, k, type(getattr(cls, k))(float(v)) if '.' in v else int(v))
 runpy.run_path('bench.py', run_name='__main__')
 '''
 
