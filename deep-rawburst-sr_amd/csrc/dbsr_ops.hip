@@ -400,6 +400,94 @@ __global__ __launch_bounds__(256) void fuse_partial_kernel(int B, int N, int hw,
     Vec4<float>::st(o + 2 * C, a);
 }
 
+// Any burst size (N > 16, beyond the register-resident kernels above): the same three passes over the
+// frames (max, sum of exp, normalised weights x features), reloading the logits per pass instead of
+// holding them in registers.  Same arithmetic and order as fuse_softmax_kernel.
+template <typename T>
+__global__ __launch_bounds__(256) void fuse_softmax_any_kernel(int B, int N, int hw, int groups, dbsr_tensor logits,
+                                                               dbsr_tensor ref, dbsr_tensor oth, dbsr_tensor fused,
+                                                               dbsr_tensor weights) {
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long long)B * hw * groups) return;
+    const int g = (int)(idx % groups);
+    const long long pix = idx / groups;
+    const int b = (int)(pix / hw), rr = (int)(pix - (long long)b * hw);
+    const int c = g * 4;
+    auto lg = [&](int n, float (&v)[4]) { Vec4<T>::ld(img_ptr<T>(logits, b * N + n) + (long long)rr * logits.ld + c, v); };
+    float m[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY}, s[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int n = 0; n < N; ++n) {
+        float l[4];
+        lg(n, l);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) m[j] = fmaxf(m[j], l[j]);
+    }
+    for (int n = 0; n < N; ++n) {
+        float l[4];
+        lg(n, l);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s[j] += __expf(l[j] - m[j]);
+    }
+    float inv[4], acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) inv[j] = 1.0f / s[j];
+    for (int n = 0; n < N; ++n) {
+        float l[4], fv[4], wn[4];
+        lg(n, l);
+        const T* fp = n == 0 ? img_ptr<T>(ref, b) + (long long)rr * ref.ld
+                             : img_ptr<T>(oth, b * (N - 1) + n - 1) + (long long)rr * oth.ld;
+        Vec4<T>::ld(fp + c, fv);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            wn[j] = __expf(l[j] - m[j]) * inv[j];
+            acc[j] = fmaf(fv[j], wn[j], acc[j]);
+        }
+        if (weights.ptr) {
+            if (weights.dtype == DBSR_F32)
+                Vec4<float>::st(img_ptr<float>(weights, b * N + n) + (long long)rr * weights.ld + c, wn);
+            else
+                Vec4<T>::st(img_ptr<T>(weights, b * N + n) + (long long)rr * weights.ld + c, wn);
+        }
+    }
+    Vec4<T>::st(img_ptr<T>(fused, b) + (long long)rr * fused.ld + c, acc);
+}
+
+// frame-sharded statistics for any burst size (two passes over the local frames)
+template <typename T>
+__global__ __launch_bounds__(256) void fuse_partial_any_kernel(int B, int N, int hw, int groups, int first,
+                                                               dbsr_tensor logits, dbsr_tensor ref, dbsr_tensor oth,
+                                                               float* __restrict__ stats) {
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long long)B * hw * groups) return;
+    const int g = (int)(idx % groups);
+    const long long pix = idx / groups;
+    const int b = (int)(pix / hw), rr = (int)(pix - (long long)b * hw);
+    const int c = g * 4, C = groups * 4;
+    float m[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY}, s[4] = {0.f, 0.f, 0.f, 0.f}, a[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int n = first; n < N; ++n) {
+        float l[4];
+        Vec4<T>::ld(img_ptr<T>(logits, b * N + n) + (long long)rr * logits.ld + c, l);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) m[j] = fmaxf(m[j], l[j]);
+    }
+    for (int n = first; n < N; ++n) {
+        float l[4], fv[4];
+        Vec4<T>::ld(img_ptr<T>(logits, b * N + n) + (long long)rr * logits.ld + c, l);
+        const T* fp = n == 0 ? img_ptr<T>(ref, b) + (long long)rr * ref.ld
+                             : img_ptr<T>(oth, b * (N - 1) + n - 1) + (long long)rr * oth.ld;
+        Vec4<T>::ld(fp + c, fv);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float e = __expf(l[j] - m[j]);
+            s[j] += e;
+            a[j] = fmaf(fv[j], e, a[j]);
+        }
+    }
+    float* o = stats + pix * 3 * C + c;
+    Vec4<float>::st(o, m);
+    Vec4<float>::st(o + C, s);
+    Vec4<float>::st(o + 2 * C, a);
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void fuse_combine_kernel(int R, int B, int hw, int groups,
                                                            const float* __restrict__ stats, dbsr_tensor fused) {
@@ -567,7 +655,7 @@ extern "C" int dbsr_fuse_softmax(int B, int N, int hw, int c, dbsr_tensor logits
     DBSR_CHECK_ARG(map_ok(logits) && map_ok(ref) && map_ok(fused) && (N == 1 || map_ok(oth)), "fuse: bad tensor");
     DBSR_CHECK_ARG(logits.dtype == ref.dtype && fused.dtype == ref.dtype && (N == 1 || oth.dtype == ref.dtype),
                    "fuse: dtype mismatch");
-    DBSR_CHECK_ARG(B > 0 && N > 0 && N <= 16 && hw > 0 && c % 4 == 0, "fuse: N must be in [1,16], c multiple of 4");
+    DBSR_CHECK_ARG(B > 0 && N > 0 && hw > 0 && c % 4 == 0, "fuse: B, N, hw > 0 and c a multiple of 4");
     DBSR_CHECK_ARG(vec_ok(logits, 4) && vec_ok(ref, 4) && vec_ok(fused, 4) && (N == 1 || vec_ok(oth, 4)),
                    "fuse: ld/c0 must be multiples of 4");
     if (weights.ptr) DBSR_CHECK_ARG(map_ok(weights) && vec_ok(weights, 4), "fuse: bad weights tensor");
@@ -575,6 +663,12 @@ extern "C" int dbsr_fuse_softmax(int B, int N, int hw, int c, dbsr_tensor logits
     const long long total = (long long)B * hw * groups;
     return by_dtype(ref.dtype, [&](auto* tag) {
         using T = std::remove_pointer_t<decltype(tag)>;
+        if (N > 16) {                   // any burst size: logits reloaded per pass
+            hipLaunchKernelGGL(fuse_softmax_any_kernel<T>, dim3(nblocks(total, 256)), dim3(256), 0,
+                               (hipStream_t)stream, B, N, hw, groups, logits, ref, oth, fused, weights);
+            DBSR_LAUNCH_CHECK();
+            return 0;
+        }
         const bool wp = groups % 64 == 0;
         if constexpr (sizeof(T) == 2) {
             if (c == 512 && vec_ok(logits, 8) && vec_ok(ref, 8) && vec_ok(fused, 8) &&
@@ -623,14 +717,17 @@ extern "C" int dbsr_fuse_partial(int B, int N, int hw, int c, int first_frame, d
                                  dbsr_tensor oth, float* stats, void* stream) {
     DBSR_CHECK_ARG(stats && map_ok(logits) && map_ok(ref) && (N == 1 || map_ok(oth)), "fuse_partial: bad tensor");
     DBSR_CHECK_ARG(logits.dtype == ref.dtype && (N == 1 || oth.dtype == ref.dtype), "fuse_partial: dtype mismatch");
-    DBSR_CHECK_ARG(B > 0 && N > 0 && N <= 16 && hw > 0 && c % 4 == 0 && first_frame >= 0 && first_frame <= N,
-                   "fuse_partial: N in [1,16], c multiple of 4, first_frame in [0,N]");
+    DBSR_CHECK_ARG(B > 0 && N > 0 && hw > 0 && c % 4 == 0 && first_frame >= 0 && first_frame <= N,
+                   "fuse_partial: B, N, hw > 0, c multiple of 4, first_frame in [0,N]");
     DBSR_CHECK_ARG(vec_ok(logits, 4) && vec_ok(ref, 4) && (N == 1 || vec_ok(oth, 4)), "fuse_partial: ld/c0 % 4");
     const int groups = c / 4;
     const long long total = (long long)B * hw * groups;
     return by_dtype(ref.dtype, [&](auto* tag) {
         using T = std::remove_pointer_t<decltype(tag)>;
-        if (N <= 8)
+        if (N > 16)
+            hipLaunchKernelGGL(fuse_partial_any_kernel<T>, dim3(nblocks(total, 256)), dim3(256), 0,
+                               (hipStream_t)stream, B, N, hw, groups, first_frame, logits, ref, oth, stats);
+        else if (N <= 8)
             hipLaunchKernelGGL((fuse_partial_kernel<T, 8>), dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream,
                                B, N, hw, groups, first_frame, logits, ref, oth, stats);
         else

@@ -149,7 +149,7 @@ std::tuple<at::Tensor, at::Tensor> fuse_softmax(const at::Tensor& logits, const 
     need_hip(logits, "fuse_softmax");
     TORCH_CHECK(logits.dim() == 5 && logits.sizes() == feats.sizes(), "dbsr::fuse_softmax: [B,N,C,H,W] inputs");
     const int64_t B = feats.size(0), N = feats.size(1), C = feats.size(2), H = feats.size(3), W = feats.size(4);
-    TORCH_CHECK(C % 4 == 0 && N <= 16, "dbsr::fuse_softmax: C % 4 == 0 and N <= 16");
+    TORCH_CHECK(C % 4 == 0, "dbsr::fuse_softmax: C % 4 == 0");
     const auto dt = feats.scalar_type();
     auto cl = [&](const at::Tensor& t) { return t.to(dt).reshape({B * N, C, H, W}).permute({0, 2, 3, 1}).contiguous(); };
     auto l = cl(logits), f = cl(feats);

@@ -10,6 +10,8 @@ device copies (layout plumbing for callers that hold NCHW tensors; the engine ne
 Errors mirror the reference: non-contiguous input to the correlation raises (correlation.py:286-287),
 a CPU tensor raises (correlation.py:324-325 raises NotImplementedError on CPU).
 """
+import collections
+
 import torch
 
 from . import _lib as L
@@ -78,6 +80,37 @@ def warp(feat, flow, mode='bilinear', padding_mode='zeros'):
     return out[..., :C].permute(0, 3, 1, 2).contiguous()
 
 
+_PACKED = collections.OrderedDict()    # (weight, bias, version, dtype, shuffle) -> packed MFMA weights
+_PACKED_MAX = 64
+
+
+def _packed(weight, bias, compute_dtype, shuffle, stream):
+    """Packed weights (dbsr_conv_pack_weights) of a parameter, cached while the tensor is unchanged (same
+    storage and autograd version counter), so a repeated op-level call does not repack."""
+    key = (weight.data_ptr(), weight._version, tuple(weight.shape),
+           bias.data_ptr() if bias is not None else 0, bias._version if bias is not None else 0,
+           compute_dtype, shuffle, weight.device)
+    hit = _PACKED.get(key)
+    if hit is not None:
+        _PACKED.move_to_end(key)
+        return hit[0], hit[1]
+    Cout, Cin, kh, kw = weight.shape
+    dev = weight.device
+    n = L.lib().dbsr_conv_packed_elems(Cout, Cin, kh, kw)
+    wp = torch.empty(n, dtype=compute_dtype, device=dev)
+    bp = torch.empty(Cout, dtype=torch.float32, device=dev) if bias is not None else None
+    w32 = weight.detach().to(torch.float32).contiguous()
+    b32 = bias.detach().to(torch.float32).contiguous() if bias is not None else None
+    L.check(L.lib().dbsr_conv_pack_weights(w32.data_ptr(), b32.data_ptr() if b32 is not None else None, Cout, Cin,
+                                           kh, kw, L.dtype_code(compute_dtype), shuffle, wp.data_ptr(),
+                                           bp.data_ptr() if bp is not None else None, stream), 'pack')
+    # the cache keeps the source tensors alive so their storage (the key) cannot be reused meanwhile
+    _PACKED[key] = (wp, bp, weight, bias, w32, b32)
+    while len(_PACKED) > _PACKED_MAX:
+        _PACKED.popitem(last=False)
+    return wp, bp
+
+
 def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, act=L.ACT_NONE, residual=None,
            post_act=L.ACT_NONE, compute_dtype=torch.float32, out_f32=False, head=None, shuffle=1):
     """act(conv2d(x) + bias) (+ residual, then post_act); NCHW in/out, computed by dbsr_conv2d.
@@ -89,15 +122,8 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, act=L.ACT_NONE
     Cout, _, kh, kw = weight.shape
     dev = x.device
     xs, ldx = _nhwc(x, compute_dtype)
-    n = L.lib().dbsr_conv_packed_elems(Cout, Cin, kh, kw)
-    wp = torch.empty(n, dtype=compute_dtype, device=dev)
-    bp = torch.empty(Cout, dtype=torch.float32, device=dev) if bias is not None else None
-    w32 = weight.to(torch.float32).contiguous()
-    b32 = bias.to(torch.float32).contiguous() if bias is not None else None
     s = L.stream_ptr(dev)
-    L.check(L.lib().dbsr_conv_pack_weights(w32.data_ptr(), b32.data_ptr() if b32 is not None else None, Cout, Cin,
-                                           kh, kw, L.dtype_code(compute_dtype), shuffle, wp.data_ptr(),
-                                           bp.data_ptr() if bp is not None else None, s), 'pack')
+    wp, bp = _packed(weight, bias, compute_dtype, shuffle, s)
     oh = (H + 2 * padding - dilation * (kh - 1) - 1) // stride + 1
     ow = (W + 2 * padding - dilation * (kw - 1) - 1) // stride + 1
     ody = torch.float32 if out_f32 else compute_dtype

@@ -90,6 +90,21 @@ def test_cfg3_burstsr_shape_fp32(synth_sd):
     assert (pred.cpu() - ref).abs().max().item() <= 1e-3
 
 
+def test_burst_longer_than_16_fp32(synth_sd):
+    """A 20-frame burst (the reference accepts any burst size, merging.py:116-124): the fusion takes the
+    any-N kernel; fp32 against the oracle at the north_star's 1e-3."""
+    from dbsr_amd.burst import synthetic_bursts
+    from oracle import dbsr_oracle as orc
+    burst, _ = synthetic_bursts(1, 20, 32, 32, sr_factor=8, seed=21)
+    net = _net(synth_sd, torch.float32)
+    with torch.no_grad():
+        pred, aux = net(burst.to(DEV))
+    ref, raux = orc.dbsr_forward(burst, synth_sd)
+    assert aux['fusion_weights'].shape[1] == 20
+    assert (aux['offsets'].cpu() - raux['offsets']).abs().max().item() <= 1e-3
+    assert (pred.cpu() - ref).abs().max().item() <= 1e-3
+
+
 def test_compute_score_hip_vs_oracle(tmp_path, synth_sd):
     """SyntheticBurstVal-layout files -> evaluation.compute_score with the HIP bf16 network (batched)
     vs the same scoring of the oracle's fp32 forward, per image within the 0.01 dB bar."""

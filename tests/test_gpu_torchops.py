@@ -55,9 +55,10 @@ def test_warp_op_and_grad(dbsr):
     assert _rel(xd.grad.cpu(), x.grad) <= 1e-5
 
 
-def test_fuse_softmax_op_and_grad(dbsr):
-    gen = torch.Generator().manual_seed(10)
-    B, N, C, H, W = 2, 4, 32, 5, 6
+@pytest.mark.parametrize('N', [4, 20])        # 20: beyond the register-resident kernels (any burst size)
+def test_fuse_softmax_op_and_grad(dbsr, N):
+    gen = torch.Generator().manual_seed(10 + N)
+    B, C, H, W = 2, 32, 5, 6
     lg = torch.randn(B, N, C, H, W, generator=gen, requires_grad=True)
     f = torch.randn(B, N, C, H, W, generator=gen, requires_grad=True)
     w = F.softmax(lg, dim=1)
