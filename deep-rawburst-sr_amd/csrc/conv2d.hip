@@ -1159,10 +1159,11 @@ struct WsCfg {
     static constexpr int STAGE_U4 = ITEMS * 64;
     static constexpr int STEPS = NCH * 9;                     // (chunk, tap) k-steps per tile
     static constexpr int DMA_STEPS = (STEPS + 1) / 2;         // the next halo goes out in the first half
-    static constexpr int RES_U4 = TW * TH * WM / 8;           // residual tile: [pixel][WM couts], 16-B slots
-    static constexpr int RES_ITEMS = RES_U4 / 64;             // its 1-KiB pieces (8 pixels x 128 B)
+    static constexpr int SPP = WM / 8;                        // 16-B slots per pixel of the residual tile
+    static constexpr int RES_U4 = TW * TH * SPP;              // residual tile: [pixel][WM couts], 16-B slots
+    static constexpr int RES_ITEMS = RES_U4 / 64;             // its 1-KiB pieces (64 / SPP pixels each)
     static constexpr int RPER = (RES_ITEMS + NWAVES - 1) / NWAVES;
-    static_assert(TH % WP == 0 && TW % 16 == 0 && WM == 64, "tile shape");
+    static_assert(TH % WP == 0 && TW % 16 == 0 && (WM == 64 || WM == 32), "tile shape");
     static_assert((2 * STAGE_U4 + 2 * RES_U4 + WM / 4) * 16 <= 160 * 1024, "halo + residual stages must fit the LDS");
 };
 
@@ -1272,8 +1273,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ws_kernel(ConvK k, int tiles_x
     };
 
     f32x4_t acc[2][C::GW];
-    // residual tile via LDS-DMA: piece q = 8 tile pixels x 128 B (64 couts); lane l -> pixel 8q + (l >> 3),
-    // physical slot l & 7 holding logical slot (l & 7) ^ (pixel & 7) -- the XOR keeps the epilogue's
+    // residual tile via LDS-DMA: piece q = 64/SPP tile pixels x WM*2 B; lane l -> pixel (64/SPP)q + l/SPP,
+    // physical slot l % SPP holding logical slot (l % SPP) ^ (pixel % SPP) -- the XOR keeps the epilogue's
     // ds_read_b128 (16 consecutive pixels x 2 slots per lane group) conflict-free.  Out-of-frame bytes
     // (a partial cout tile at the frame's last pixel) land zeros.
     // the resource spans the residual frame from its first channel, so the slots of a partial cout tile
@@ -1282,7 +1283,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ws_kernel(ConvK k, int tiles_x
     const int r_cb = k.r_c0 + ct * WM;
     auto res_dma = [&](int it, const Tile& t, int buf) {
         const int q = min(wave + C::NWAVES * it, C::RES_ITEMS - 1);
-        const int pp = q * 8 + (lane >> 3), ls = (lane & 7) ^ (pp & 7);
+        const int pp = q * (64 / C::SPP) + lane / C::SPP, ls = (lane % C::SPP) ^ (pp % C::SPP);
         const int off = (((t.y0 + pp / TW) * k.out_w + t.x0 + pp % TW) * k.r_ld + r_cb + ls * 8) * (int)sizeof(T);
         blds16(buf_rsrc((const T*)k.r + t.r_off, rframe_bytes), off, 0, lres + buf * C::RES_U4 + q * 64);
     };
@@ -1300,7 +1301,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ws_kernel(ConvK k, int tiles_x
             }
             if (has_res) {
                 const int pp = (wp * C::RPW + j / C::GPR) * TW + (j % C::GPR) * 16 + col;
-                const u32x4_t rq = lres[rbuf * C::RES_U4 + pp * 8 + ((wc * 4 + g) ^ (pp & 7))];
+                const u32x4_t rq = lres[rbuf * C::RES_U4 + pp * C::SPP + ((wc * 4 + g) ^ (pp % C::SPP))];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     v[2 * e] = act2(v[2 * e] + H16<T>::lo(rq[e]));
@@ -1386,19 +1387,25 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ws_kernel(ConvK k, int tiles_x
 
 int g_ws_enabled = 1;
 // weight-stationary kernel for `d` (blocks per XCD, 0: not applicable): 16-bit 3x3/s1/p1/d1 with
-// 32 < cout <= 512 and 16 < cin <= 64, 16x16-divisible frames, aligned NHWC output / residual
+// either 16 < cin <= 64, 32 < cout <= 512 on 16x16 tiles (WM 64) or 16 < cin <= 32, 16 <= cout <= 32 on 64x8
+// tiles (WM 32: the decoder's 384x384 post-ResBlocks), aligned NHWC output / residual
+inline bool ws_narrow(const dbsr_conv_desc* d) { return d->cout <= 32; }
 int pick_ws(const dbsr_conv_desc* d) {
     if (!g_ws_enabled || !is16(d->x.dtype) || d->precise || d->kh != 3 || d->kw != 3 || d->stride != 1 ||
         d->pad != 1 || d->dil != 1 || d->cin <= 16 || d->cin > 64 || d->out_mode != DBSR_OUT_NHWC ||
         d->y.dtype != d->x.dtype || d->gate.ptr)
         return 0;
-    if (d->y.ld % 8 || d->y.c0 % 8 || d->cout % 8 || d->cout <= 32 || d->cout > 512 ||
+    if (d->y.ld % 8 || d->y.c0 % 8 || d->cout % 8 || d->cout > 512 ||
         (d->res.ptr && (d->res.ld % 8 || d->res.c0 % 8)))
         return 0;
-    if (d->out_w % 16 || d->out_h % 16) return 0;
+    const bool narrow = ws_narrow(d);
+    const int tw = narrow ? 64 : 16, th = narrow ? 8 : 16, wm = narrow ? 32 : 64;
+    if (narrow && (d->cout < 16 || d->cin > 32)) return 0;      // WM 32: one 32-channel chunk (LDS budget)
+    if (d->out_w % tw || d->out_h % th) return 0;
     if ((long long)d->in_h * d->in_w * d->x.ld * 2 >= (1LL << 31)) return 0;   // 32-bit buffer offsets per frame
-    const int nct = (d->cout + 63) / 64;
-    const long long nsp = (long long)d->n_frames * (d->out_w / 16) * (d->out_h / 16);
+    if (d->res.ptr && (long long)d->out_h * d->out_w * d->res.ld * 2 >= (1LL << 31)) return 0;
+    const int nct = (d->cout + wm - 1) / wm;
+    const long long nsp = (long long)d->n_frames * (d->out_w / tw) * (d->out_h / th);
     const int cus = d->max_blocks > 0 ? std::min(d->max_blocks, num_cus()) : num_cus();
     const long long want = (nsp + 7) / 8;                                      // spatial streams per XCD
     const long long spx = std::min<long long>(cus / 8 / nct, want);
@@ -1406,17 +1413,17 @@ int pick_ws(const dbsr_conv_desc* d) {
     return (int)(spx * nct);
 }
 
-template <typename T, int NCH>
+template <typename T, int WM, int TW, int TH, int NCH>
 int launch_ws(const ConvK& k, const dbsr_conv_desc* d, int px, hipStream_t s) {
-    const int tiles_x = k.out_w / 16, tiles_y = k.out_h / 16;
-    const int nct = (k.cout + 63) / 64;
+    const int tiles_x = k.out_w / TW, tiles_y = k.out_h / TH;
+    const int nct = (k.cout + WM - 1) / WM;
     const int nsp = d->n_frames * tiles_x * tiles_y;
     int epi = 0;
     if (!k.r && k.act == DBSR_ACT_RELU) epi = 1;
     else if (k.r && k.act == DBSR_ACT_NONE && k.post_act == DBSR_ACT_RELU) epi = 2;
     else if (!k.r && k.act == DBSR_ACT_NONE) epi = 3;
 #define DBSR_WS_LAUNCH(E)                                                                                         \
-    hipLaunchKernelGGL((conv3x3_ws_kernel<T, 64, 16, 16, NCH, E>), dim3(8 * px), dim3(512), 0, s, k, tiles_x,    \
+    hipLaunchKernelGGL((conv3x3_ws_kernel<T, WM, TW, TH, NCH, E>), dim3(8 * px), dim3(512), 0, s, k, tiles_x,    \
                        tiles_y, nct, nsp, px)
     switch (epi) {
         case 1: DBSR_WS_LAUNCH(1); break;
@@ -1431,8 +1438,9 @@ int launch_ws(const ConvK& k, const dbsr_conv_desc* d, int px, hipStream_t s) {
 
 template <typename T>
 int dispatch_ws(int px, const ConvK& k, const dbsr_conv_desc* d, hipStream_t s) {
-    if (k.CG / 4 == 1) return launch_ws<T, 1>(k, d, px, s);
-    return launch_ws<T, 2>(k, d, px, s);
+    if (ws_narrow(d)) return launch_ws<T, 32, 64, 8, 1>(k, d, px, s);
+    if (k.CG / 4 == 1) return launch_ws<T, 64, 16, 16, 1>(k, d, px, s);
+    return launch_ws<T, 64, 16, 16, 2>(k, d, px, s);
 }
 
 template <typename T>

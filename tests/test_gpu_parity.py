@@ -176,13 +176,22 @@ WS_EPI = [
 ]
 
 
-@pytest.mark.parametrize('case', WS_EPI)
+# the 32-cout variant on 64x8 tiles (the decoder's 384x384 post-ResBlocks): act, residual, post, cin, cout, dtype
+WS32_EPI = [
+    (1, False, 0, 32, 32, torch.bfloat16), (0, True, 1, 32, 32, torch.bfloat16), (0, False, 0, 32, 32, torch.bfloat16),
+    (1, False, 0, 24, 16, torch.bfloat16), (0, True, 1, 32, 24, torch.float16), (2, True, 1, 32, 32, torch.float16),
+]
+
+
+@pytest.mark.parametrize('case', WS_EPI + WS32_EPI)
 def test_ws_conv_variants(ops_mod, case):
     """Weight-stationary 3x3 conv against torch on the same 16-bit-rounded operands, and against the
-    generic kernel; frames 48x48 (the encoder's) and 32x16 (non-square, edge tiles on both axes)."""
+    generic kernel; WM 64: frames 48x48 (the encoder's) and 32x16 (non-square, edge tiles on both axes);
+    WM 32 (cout <= 32, 64x8 tiles): 64x64 and 48x192 frames."""
     from dbsr_amd import _lib
     act, use_res, post, cin, cout, dt = case
-    for (N, H, W) in ((12, 48, 48), (40, 32, 16)):
+    shapes = ((12, 48, 48), (40, 32, 16)) if cout > 32 else ((8, 64, 64), (4, 48, 192))
+    for (N, H, W) in shapes:
         gen = torch.Generator().manual_seed(cin * 13 + cout + act * 7 + post + H)
         x = torch.randn(N, cin, H, W, generator=gen)
         w = torch.randn(cout, cin, 3, 3, generator=gen) / (cin * 9) ** 0.5
