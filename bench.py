@@ -179,11 +179,16 @@ def main():
     kdesc = {'conv3x3_ws': 'conv3x3_ws_kernel (persistent weight-stationary implicit-GEMM 3x3, Cin <= 64',
              'conv3x3_pipe': 'conv3x3_pipe_kernel (persistent LDS-DMA-pipelined implicit-GEMM 3x3',
              'conv3x3_tiled': 'conv3x3_tiled_kernel (LDS-tiled implicit-GEMM 3x3',
-             'conv2d_generic': 'conv2d_kernel (generic implicit-GEMM'}[dom]
+             'conv2d_generic': 'conv2d_kernel (generic implicit-GEMM',
+             'conv_fuse': 'conv_fuse_kernel (weight-predictor output conv + softmax + fusion'}[dom]
     roof = {'bound': 'mfma', 'kernel': kdesc + ', %d launches per forward; '
                                        'achieved = their algorithmic FLOPs / their summed event-timed durations)' % t_n,
             'achieved': round(t_tf, 2), 'peak': peak_t, 'unit': 'TFLOP/s', 'frac': round(t_tf / peak_t, 4),
             'traffic': None}
+    # every conv family against the same dense peak (the roofline object above is the dominant one)
+    fam_roof = {k: {'achieved_tflops': round(w / (ms * 1e-3) / 1e12, 2), 'frac': round(w / (ms * 1e-3) / 1e12 / peak_t, 4),
+                    'ms': round(ms, 4), 'launches': n}
+                for k, (ms, w, n) in fam.items() if k.startswith('conv') and ms > 0}
     conv_ms = sum(ms for kind, (ms, w, n) in fam.items() if kind.startswith('conv'))
     conv_n = sum(n for kind, (ms, w, n) in fam.items() if kind.startswith('conv'))
     all_conv_tf = conv_flop / (conv_ms * 1e-3) / 1e12
@@ -225,6 +230,7 @@ def main():
                        'parallelism': 'dp%d (independent bursts per rank)' % world,
                        'hip_graph': not args.no_graph, 'fusion_weights_written': True},
             'roofline': roof, 'roofline_hbm': hbm,
+            'roofline_families': fam_roof,
             'conv_all': {'achieved_tflops': round(all_conv_tf, 2), 'launches': conv_n,
                          'ms_by_kernel': {k: round(v[0], 3) for k, v in fam.items() if k.startswith('conv')}},
             'cpu_baseline': cpu,
