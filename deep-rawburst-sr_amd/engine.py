@@ -18,7 +18,9 @@ Layout map (reference file:line per stage):
                            reads a channel suffix, so torch.cat never happens (pwcnet.py:173-177)
   E       [F,H,W,512]      frame embeddings                         encoders.py:66-72
   Wf      [P,H,W,512]      warped embeddings of frames 1..N-1      encoders.py:80
-  LG      [F,H,W,512]      fusion logits                            merging.py:113
+  WP      [F,H,W,128]      weight-predictor input [proj | offfeat]  merging.py:77-110 (linearity split:
+                           the base term is BS [B,H,W,128], one conv per burst, merging.py:87-89)
+  LG      [F,H,W,512]      fusion logits (not with FUSED_WP_OUT)    merging.py:113
   FW      [F,H,W,512]      fusion weights (aux output)              merging.py:118
   FUS     [B,H,W,512]      fused embedding                          merging.py:124
   S*      [B,sH,sW,32]     post-upsampler features                  decoders.py:58-60
