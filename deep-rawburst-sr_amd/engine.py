@@ -586,9 +586,24 @@ class DBSREngine:
         plan.keep.extend([WP, o])
         return WP
 
-    def _emit_merge(self, plan, grp, N, H, W, sh, WP):
+    def _emit_base(self, plan, grp, N, H, W, sh, WP):
+        """Linearity split: the reference frames' projection into WP[..., :pd] and the per-burst base conv
+        (merging.py:77-89).  Needs only the encoder, so the first group's runs on lane 0 beside the
+        alignment chain; returns the base-term buffer BS."""
+        g0, g1 = grp
+        Bg = g1 - g0
+        rest, basec = self.wp_split
+        plan.conv('merge.proj_ref', self.proj, Bg, sh['E'], 0, (H, W), WP, 0, L.ACT_RELU, xmap=(1, N, g0 * N, 1),
+                  ymap=(1, N, 0, 1))
+        BS = NHWC(Bg, H, W, r8(basec.cout), self.dtype, self.device)
+        plan.conv('merge.wp.base', basec, Bg, WP, 0, (H, W), BS, 0, L.ACT_NONE, xmap=(1, N, 0, 1))
+        plan.keep.append(BS)
+        return BS
+
+    def _emit_merge(self, plan, grp, N, H, W, sh, WP, BS=None):
         """Warp (encoders.py:80) + projections, weight predictor (merging.py:61-113) of the group; returns
-        the logits LG and the warped embeddings Wf."""
+        the weight predictor's last hidden buffer and the warped embeddings Wf.  BS: the group's base term
+        if _emit_base already ran."""
         dt, dev = self.dtype, self.device
         lib = L.lib()
         g0, g1 = grp
@@ -607,16 +622,13 @@ class DBSREngine:
         if self.wp_split is not None:
             # projections straight into WP[..., :pd]; the base term once per burst, added (broadcast over the
             # burst's frames) as the residual of the per-frame conv before its ReLU
-            rest, basec = self.wp_split
-            plan.conv('merge.proj_ref', self.proj, Bg, E, 0, hw, WP, 0, L.ACT_RELU, xmap=(1, N, off_f, 1),
-                      ymap=(1, N, 0, 1))
+            rest = self.wp_split[0]
+            if BS is None:
+                BS = self._emit_base(plan, grp, N, H, W, sh, WP)
             if Pg > 0:
                 plan.conv('merge.proj_oth', self.proj, Pg, Wf, 0, hw, WP, 0, L.ACT_RELU, ymap=(N - 1, N, 1, 1))
-            BS = NHWC(Bg, H, W, r8(basec.cout), dt, dev)
-            plan.conv('merge.wp.base', basec, Bg, WP, 0, hw, BS, 0, L.ACT_NONE, xmap=(1, N, 0, 1))
             plan.conv('merge.wp.init', rest, Fg, WP, 0, hw, q[0], 0, L.ACT_NONE, res=BS, rmap=(N, 1, 0, 0),
                       post_act=L.ACT_RELU)
-            plan.keep.append(BS)
         else:
             if Pg > 0:
                 plan.conv('merge.proj_oth', self.proj, Pg, Wf, 0, hw, PJ, 0, L.ACT_RELU,
@@ -683,6 +695,9 @@ class DBSREngine:
             bufs['pred'] = torch.zeros(B, 3, H * self.s, W * self.s, dtype=torch.float32, device=dev)
         plan.fuse_ops = []
         es = 4 if dt == torch.float32 else 2
+        # the first group's base term needs only the encoder: lane 0 computes it before waiting for PWC-Net
+        # (its projections write WP channels [0, pd); the side lane writes the offset features at [pd, ..))
+        BS0 = self._emit_base(plan, groups[0], N, H, W, sh, WPs[0]) if self.wp_split is not None else None
         for gi, grp in enumerate(groups):
             plan.join(1)                      # lane 0 waits for this group's alignment chain
             if gi + 1 < len(groups):
@@ -692,7 +707,7 @@ class DBSREngine:
                 plan.max_blocks = plan_cap
             else:
                 plan.max_blocks = 0
-            h, Wf = self._emit_merge(plan, grp, N, H, W, sh, WPs[gi])
+            h, Wf = self._emit_merge(plan, grp, N, H, W, sh, WPs[gi], BS=BS0 if gi == 0 else None)
             g0, g1 = grp
             Bg = g1 - g0
             if mode == 'partial':
