@@ -546,7 +546,14 @@ class DBSREngine:
 
     def _emit_align(self, plan, grp, N, H, W, sh):
         """PWC-Net flow of the group's pairs -> offsets / offset features (flow_finalize) -> offset-feature
-        extractor (merging.py:85-87) -> WP[..., 2*pd:] of the group."""
+        extractor (merging.py:85-87) -> WP[..., oc:] of the group."""
+        WP = self._emit_flow(plan, grp, N, H, W, sh)
+        self._emit_ofe(plan, grp, N, H, W, sh, WP)
+        return WP
+
+    def _emit_flow(self, plan, grp, N, H, W, sh):
+        """PWC-Net flow of the group's pairs -> offsets and the offset-feature input (flow_finalize); returns
+        the group's (still empty) weight-predictor input buffer WP."""
         dt, dev = self.dtype, self.device
         lib = L.lib()
         g0, g1 = grp
@@ -567,6 +574,18 @@ class DBSREngine:
         # weight-predictor input: [base, diff, offfeat] (merging.py:110), or [proj, offfeat] with the split
         oc = pd if self.wp_split is not None else 2 * pd
         WP = NHWC(Fg, H, W, oc + od, dt, dev)
+        plan.keep.append(WP)
+        return WP
+
+    def _emit_ofe(self, plan, grp, N, H, W, sh, WP):
+        """Offset-feature extractor (merging.py:85-87) of the group -> WP[..., oc:]."""
+        dt, dev = self.dtype, self.device
+        g0, g1 = grp
+        Fg = (g1 - g0) * N
+        fmap = (1, 1, g0 * N, 0)
+        hw = (H, W)
+        pd, od = self.proj.cout, self.ofe_init.cout
+        oc = pd if self.wp_split is not None else 2 * pd
         o = [NHWC(Fg, H, W, od, dt, dev) for _ in range(3)]
         plan.conv('merge.ofe.init', self.ofe_init, Fg, sh['om'], 0, hw, o[0], 0, L.ACT_RELU, xmap=fmap)
         a = 0
@@ -583,8 +602,7 @@ class DBSREngine:
                 plan.conv(f'merge.ofe.res{k}.conv2', c2, Fg, o[b], 0, hw, o[c], 0, L.ACT_NONE, res=o[a],
                           post_act=L.ACT_RELU)
                 a = c
-        plan.keep.extend([WP, o])
-        return WP
+        plan.keep.append(o)
 
     def _emit_base(self, plan, grp, N, H, W, sh, WP):
         """Linearity split: the reference frames' projection into WP[..., :pd] and the per-burst base conv
@@ -600,33 +618,46 @@ class DBSREngine:
         plan.keep.append(BS)
         return BS
 
-    def _emit_merge(self, plan, grp, N, H, W, sh, WP, BS=None):
+    def _emit_warp(self, plan, grp, N, H, W, sh, WP):
+        """Warp of the group's other frames (encoders.py:80) and, with the linearity split, their projection
+        straight into WP[..., :pd] (merging.py:77): needs the offsets, not the offset features."""
+        dt, dev = self.dtype, self.device
+        g0, g1 = grp
+        Pg = (g1 - g0) * (N - 1)
+        off_f, off_p = g0 * N, g0 * (N - 1)
+        C, E = self.enc_out.cout, sh['E']
+        Wf = NHWC(max(Pg, 1), H, W, C, dt, dev)
+        es = 4 if dt == torch.float32 else 2
+        if Pg > 0:
+            plan.add('warp', L.lib().dbsr_warp_bilinear, Pg, H, W, C, E.d(0, (N - 1, N, 1 + off_f, 1)),
+                     sh['offsets'][off_p:].data_ptr(), 2 * H * W, Wf.d(0),
+                     work=('byte', 2.0 * Pg * C * H * W * es + 8.0 * Pg * H * W))
+            if self.wp_split is not None:
+                plan.conv('merge.proj_oth', self.proj, Pg, Wf, 0, (H, W), WP, 0, L.ACT_RELU, ymap=(N - 1, N, 1, 1))
+        plan.keep.append(Wf)
+        return Wf
+
+    def _emit_merge(self, plan, grp, N, H, W, sh, WP, BS=None, Wf=None):
         """Warp (encoders.py:80) + projections, weight predictor (merging.py:61-113) of the group; returns
-        the weight predictor's last hidden buffer and the warped embeddings Wf.  BS: the group's base term
-        if _emit_base already ran."""
+        the weight predictor's last hidden buffer and the warped embeddings Wf.  BS / Wf: the group's base
+        term / warped frames (with their projections) if _emit_base / _emit_warp already ran."""
         dt, dev = self.dtype, self.device
         lib = L.lib()
         g0, g1 = grp
         Bg, Fg, Pg = g1 - g0, (g1 - g0) * N, (g1 - g0) * (N - 1)
-        off_f, off_p = g0 * N, g0 * (N - 1)
-        C, E, PJ = self.enc_out.cout, sh['E'], sh['PJ']
+        off_f = g0 * N
+        PJ = sh['PJ']
         hw = (H, W)
         pd = self.proj.cout
-        Wf = NHWC(max(Pg, 1), H, W, C, dt, dev)
-        es = 4 if dt == torch.float32 else 2
-        if Pg > 0:
-            plan.add('warp', lib.dbsr_warp_bilinear, Pg, H, W, C, E.d(0, (N - 1, N, 1 + off_f, 1)),
-                     sh['offsets'][off_p:].data_ptr(), 2 * H * W, Wf.d(0),
-                     work=('byte', 2.0 * Pg * C * H * W * es + 8.0 * Pg * H * W))
+        if Wf is None:
+            Wf = self._emit_warp(plan, grp, N, H, W, sh, WP)
         q = [NHWC(Fg, H, W, self.wp_init.cout, dt, dev) for _ in range(3)]
         if self.wp_split is not None:
-            # projections straight into WP[..., :pd]; the base term once per burst, added (broadcast over the
-            # burst's frames) as the residual of the per-frame conv before its ReLU
+            # the base term once per burst, added (broadcast over the burst's frames) as the residual of the
+            # per-frame [proj, offfeat] conv before its ReLU
             rest = self.wp_split[0]
             if BS is None:
                 BS = self._emit_base(plan, grp, N, H, W, sh, WP)
-            if Pg > 0:
-                plan.conv('merge.proj_oth', self.proj, Pg, Wf, 0, hw, WP, 0, L.ACT_RELU, ymap=(N - 1, N, 1, 1))
             plan.conv('merge.wp.init', rest, Fg, WP, 0, hw, q[0], 0, L.ACT_NONE, res=BS, rmap=(N, 1, 0, 0),
                       post_act=L.ACT_RELU)
         else:
@@ -636,7 +667,7 @@ class DBSREngine:
             plan.add('merge.prep', lib.dbsr_merge_prep, Bg, N, H * W, pd, PJ.d(0, (1, 1, off_f, 0)), WP.d(0))
             plan.conv('merge.wp.init', self.wp_init, Fg, WP, 0, hw, q[0], 0, L.ACT_RELU)
         i = self._resblocks(plan, 'merge.wp.res', self.wp_res, Fg, hw, q, 0, dt)
-        plan.keep.extend([Wf, q])
+        plan.keep.append(q)
         return q[i], Wf
 
     def _emit_logits(self, plan, Fg, H, W, h):
@@ -678,7 +709,11 @@ class DBSREngine:
         plan_cap = int(torch.cuda.get_device_properties(dev).multi_processor_count * DBSREngine.LANE0_CU_SHARE) \
             if Plan.MULTI_STREAM else 0
         plan.fork(1, dev, priority=-1)
-        WPs = [self._emit_align(plan, groups[0], N, H, W, sh)]
+        # one burst group: the offset-feature extractor waits on lane 1 until lane 0 has joined the flow, so it
+        # runs beside the warp + projections instead of before them
+        split_ofe = len(groups) == 1
+        WPs = [self._emit_flow(plan, groups[0], N, H, W, sh) if split_ofe else
+               self._emit_align(plan, groups[0], N, H, W, sh)]
         plan.switch(0)
         plan.max_blocks = plan_cap
         # ---------------- encoder (encoders.py:66-72), whole batch ----------------
@@ -707,7 +742,14 @@ class DBSREngine:
                 plan.max_blocks = plan_cap
             else:
                 plan.max_blocks = 0
-            h, Wf = self._emit_merge(plan, grp, N, H, W, sh, WPs[gi], BS=BS0 if gi == 0 else None)
+            Wf = None
+            if split_ofe:
+                plan.switch(1)                # offsets are in: offset features on lane 1 ...
+                self._emit_ofe(plan, grp, N, H, W, sh, WPs[gi])
+                plan.switch(0)
+                Wf = self._emit_warp(plan, grp, N, H, W, sh, WPs[gi])   # ... beside the warp + projections
+                plan.join(1)
+            h, Wf = self._emit_merge(plan, grp, N, H, W, sh, WPs[gi], BS=BS0 if gi == 0 else None, Wf=Wf)
             g0, g1 = grp
             Bg = g1 - g0
             if mode == 'partial':
