@@ -236,44 +236,11 @@ class Plan:
             for d in ds:
                 d.workspace, d.workspace_bytes = self.ws[lane].data_ptr(), need
 
-    # Issue the ops of concurrent lanes interleaved (see issue_order)
-    INTERLEAVE_LANES = True
-
-    def issue_order(self):
-        """Indices of self.ops in issue order.  Between consecutive fork / join entries the ops of different
-        lanes are independent, so they are interleaved in proportion to their counts: a HIP graph submits its
-        kernel nodes in creation order at ~10 us each (rocprofv3 trace), so a lane whose ops were
-        all created after the other lane's ~60 PWC-Net launches would start ~0.8 ms late."""
-        if not Plan.INTERLEAVE_LANES:
-            return list(range(len(self.ops)))
-        order, seg = [], []
-
-        def flush():
-            by = {}
-            for i in seg:
-                by.setdefault(self.ops[i][3], []).append(i)
-            lists = list(by.values())
-            pos = [0] * len(lists)
-            for _ in range(len(seg)):
-                k = min((j for j in range(len(lists)) if pos[j] < len(lists[j])),
-                        key=lambda j: (pos[j] + 0.5) / len(lists[j]))
-                order.append(lists[k][pos[k]])
-                pos[k] += 1
-            seg.clear()
-        for i, (fn, _, _, _) in enumerate(self.ops):
-            if fn is Plan.FORK or fn is Plan.JOIN:
-                flush()
-                order.append(i)
-            else:
-                seg.append(i)
-        flush()
-        return order
-
     def run(self, stream):
         main = torch.cuda.current_stream()
         if self.streams:
             assert main.cuda_stream == stream, 'Plan.run: lanes fork from the current stream'
-        for fn, args, name, lane in (self.ops[i] for i in self.issue_order()):
+        for fn, args, name, lane in self.ops:
             if fn is Plan.FORK:
                 args[0].record(main)
                 self.streams[lane].wait_event(args[0])
