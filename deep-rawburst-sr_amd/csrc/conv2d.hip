@@ -1164,7 +1164,10 @@ struct WsCfg {
     static constexpr int RES_ITEMS = RES_U4 / 64;             // its 1-KiB pieces (64 / SPP pixels each)
     static constexpr int RPER = (RES_ITEMS + NWAVES - 1) / NWAVES;
     static_assert(TH % WP == 0 && TW % 16 == 0 && (WM == 64 || WM == 32), "tile shape");
+    static constexpr int W_PIECES = (WM / 16) * NCH * 9;      // the cout tile's chunk-major weights, 1-KiB pieces
+    static constexpr int W_PER = (W_PIECES + NWAVES - 1) / NWAVES;
     static_assert((2 * STAGE_U4 + 2 * RES_U4 + WM / 4) * 16 <= 160 * 1024, "halo + residual stages must fit the LDS");
+    static_assert((STAGE_U4 + W_PIECES * 64 + WM / 4) * 16 <= 160 * 1024, "weight staging must fit the LDS");
 };
 
 template <typename T, int WM, int TW, int TH, int NCH, int EPI>
@@ -1177,9 +1180,14 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ws_kernel(ConvK k, int tiles_x
     // the next tile's halo goes out over the first half of the k-steps when the residual follows in the
     // second half, else over the first two thirds (measured: enc.out 205 -> 196 us, residual convs slower)
     constexpr int DMA_STEPS = RES_BUFS > 0 ? C::DMA_STEPS : (2 * C::STEPS) / 3;
-    __shared__ __attribute__((aligned(16))) u32x4_t lds[2 * C::STAGE_U4 + RES_BUFS * C::RES_U4 + WM / 4];
+    // [halo 0][halo 1][residual 0][residual 1][bias]; at the start the block's weights are staged once at
+    // [halo 1 ...) (every wave then copies its A-fragments to registers) instead of each of the 8 waves
+    // fetching its fragments from L2 (4 waves share each fragment set)
+    constexpr int BUF_U4 = 2 * C::STAGE_U4 + RES_BUFS * C::RES_U4;
+    constexpr int STG_U4 = C::STAGE_U4 + C::W_PIECES * 64;
+    __shared__ __attribute__((aligned(16))) u32x4_t lds[(BUF_U4 > STG_U4 ? BUF_U4 : STG_U4) + WM / 4];
     u32x4_t* lres = lds + 2 * C::STAGE_U4;                 // residual tiles (double-buffered)
-    float* lbias = (float*)(lres + RES_BUFS * C::RES_U4);  // the cout tile's bias (fp32)
+    float* lbias = (float*)(lds + (BUF_U4 > STG_U4 ? BUF_U4 : STG_U4));   // the cout tile's bias (fp32)
 
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int g = lane >> 4, col = lane & 15;
@@ -1203,16 +1211,17 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ws_kernel(ConvK k, int tiles_x
     if (my_tiles == 0) return;
     PIPE_STAMP(0);
 
-    // the wave's weights: A-fragments of both 16-cout blocks for every (chunk, tap), chunk-major copy
+    // the cout tile's weights (chunk-major copy: contiguous 1-KiB pieces) into the staging region
     const int cb = ct * WM + wc * 32;
-    Frag<T> wr[NCH][9][2];
+    {
+        const __amdgpu_buffer_rsrc_t w_rsrc = buf_rsrc(k.w_pipe, 0xffffffffu);
+        const int p0 = (ct * WM >> 4) * NCH * 9;
 #pragma unroll
-    for (int c = 0; c < NCH; ++c)
-#pragma unroll
-        for (int tap = 0; tap < 9; ++tap)
-#pragma unroll
-            for (int h = 0; h < 2; ++h)
-                wr[c][tap][h].load((const T*)k.w_pipe + ((((cb >> 4) + h) * NCH + c) * 9 + tap) * 512 + lane * 8);
+        for (int it = 0; it < C::W_PER; ++it) {
+            const int piece = min(wave + C::NWAVES * it, C::W_PIECES - 1);
+            blds16(w_rsrc, lane * 16, (p0 + piece) * 1024, lds + C::STAGE_U4 + piece * 64);
+        }
+    }
     if (threadIdx.x < WM) {             // ordered before its first read by the loop's first barrier
         const int co = ct * WM + threadIdx.x;
         lbias[threadIdx.x] = (k.bias && co < k.cout) ? k.bias[co] : 0.f;
@@ -1321,12 +1330,19 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ws_kernel(ConvK k, int tiles_x
     Tile cur = decode(0), prev = cur;
 #pragma unroll
     for (int it = 0; it < C::PER; ++it) dma(it, cur, 0);
-    if constexpr (RES_BUFS > 0) {
-        if (has_res) {
+    // the wave's A-fragments of both 16-cout blocks for every (chunk, tap), from the staged weights; the
+    // loop's first barrier then orders these reads before any wave's DMA into the staging region
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    Frag<T> wr[NCH][9][2];
 #pragma unroll
-            for (int it = 0; it < C::RPER; ++it) res_dma(it, cur, 0);
-        }
-    }
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                wr[c][tap][h].v = __builtin_bit_cast(
+                    bf16x8_t, lds[C::STAGE_U4 + (((wc * 2 + h) * NCH + c) * 9 + tap) * 64 + lane]);
 
     PIPE_STAMP(2);
     for (int ti = 0; ti < my_tiles; ++ti) {
@@ -1356,6 +1372,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ws_kernel(ConvK k, int tiles_x
                     if ((it * DMA_STEPS) / C::PER == step) dma(it, nxt, nbuf);
             }
             if constexpr (RES_BUFS > 0) {
+                if (has_res && ti == 0) {      // tile 0's residual (its buffer was the weight staging area)
+#pragma unroll
+                    for (int it = 0; it < C::RPER; ++it)
+                        if (it == step) res_dma(it, cur, 0);
+                }
                 if (has_res && more) {
 #pragma unroll
                     for (int it = 0; it < C::RPER; ++it)
