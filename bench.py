@@ -180,6 +180,8 @@ def main():
              'conv3x3_pipe': 'conv3x3_pipe_kernel (persistent LDS-DMA-pipelined implicit-GEMM 3x3',
              'conv3x3_tiled': 'conv3x3_tiled_kernel (LDS-tiled implicit-GEMM 3x3',
              'conv2d_generic': 'conv2d_kernel (generic implicit-GEMM',
+             'conv1x1': 'conv1x1_kernel (pointwise projection, LDS-resident weights',
+             'conv1x1_shuffle': 'upsample_shuffle_kernel (1x1 conv + PixelShuffle',
              'conv_fuse': 'conv_fuse_kernel (weight-predictor output conv + softmax + fusion'}[dom]
     roof = {'bound': 'mfma', 'kernel': kdesc + ', %d launches per forward; '
                                        'achieved = their algorithmic FLOPs / their summed event-timed durations)' % t_n,

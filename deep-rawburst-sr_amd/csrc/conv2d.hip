@@ -1714,6 +1714,125 @@ int launch_upsample(const ConvK& k, hipStream_t s) {
     return 0;
 }
 
+// ------------------------------------------------------------------------------------------------
+// Pointwise (1x1) projection: the merge's feat_project_layer (merging.py:34, 75: 1x1 conv 512 -> 64
+// + ReLU over every frame's embedding).  HBM-bound (1 KB read per pixel, 128 B written): the kernel
+// reads each pixel once with 16-B loads and never touches the weights in HBM after the prologue.
+// Block = 8 waves.  The whole weight matrix (cout x Kp, <= 64 KB) is copied once per block into the
+// LDS, 16-B chunk (row c, chunk q) at row c, position q ^ key(c) (key(c) = the MFMA row lane col that
+// reads row c, so the 16 rows of one A fragment hit 16 distinct bank groups).  Each wave then takes
+// groups of PG*16 pixels independently (no barriers): loads all PG x KS B-fragments of its pixels
+// (16 KB in flight per wave at PG 1, Kp 512), runs CT x 2 x PG x KS MFMAs against A fragments read
+// from the LDS, and stores 8 contiguous channels per lane (rows ordered c = 8(m>>2) + 4h + (m&3) as
+// in upsample_shuffle_kernel).  16-bit, cin % 32 == 0, cout % 32 == 0, cout * cin <= 32768.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ int pw_key(int c) { return (c & 3) | ((c >> 1) & 12); }
+
+template <typename T, int CT, int KS, int PG, int NW>
+__global__ __launch_bounds__(NW * 64, PG == 1 ? 4 : 2) void conv1x1_kernel(ConvK k, int ngroups) {
+    constexpr int KQ = KS * 4;                            // 16-B chunks per weight row
+    __shared__ __attribute__((aligned(16))) u32x4_t pw_lds[CT * 32 * KQ];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int g = lane >> 4, col = lane & 15;
+    for (int i = threadIdx.x; i < CT * 32 * KQ; i += NW * 64) {
+        const int c = i / KQ, q = i - c * KQ;
+        pw_lds[c * KQ + (q ^ pw_key(c))] = *((const u32x4_t*)k.w + (long long)c * (k.Kp / 8) + q);
+    }
+    __syncthreads();
+    const int hw = k.out_h * k.out_w;
+    f32x4_t bias[CT][2];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) bias[ct][h] = load_bias4(k, ct * 32 + 8 * g + 4 * h);
+    for (int grp = blockIdx.x * NW + wave; grp < ngroups; grp += gridDim.x * NW) {
+        Frag<T> b[PG][KS];
+        int pf[PG], prr[PG];
+#pragma unroll
+        for (int j = 0; j < PG; ++j) {
+            const int p = grp * (PG * 16) + j * 16 + col;
+            const bool ok = p < k.npix;
+            const int f = ok ? p / hw : 0, rr = ok ? p - f * hw : 0;
+            pf[j] = ok ? f : -1;
+            prr[j] = rr;
+            const T* xp = (const T*)k.x + map_frame(k.xm, f) * k.x_is + (long long)rr * k.x_ld + g * 8;
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                if (ok) b[j][ks].load(xp + ks * 32);
+                else b[j][ks].zero();
+            }
+        }
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+            f32x4_t acc[2][PG];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                int c = ct * 32 + 8 * (col >> 2) + 4 * h + (col & 3);
+                asm volatile("" : "+v"(c));            // keep the A reads in the loop (hoisted: 4 VGPRs per read)
+                const u32x4_t* arow = pw_lds + c * KQ;
+                const int key = pw_key(c);
+#pragma unroll
+                for (int j = 0; j < PG; ++j) acc[h][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks) {
+                    Frag<T> a;
+                    a.v = __builtin_bit_cast(bf16x8_t, arow[(ks * 4 + g) ^ key]);
+#pragma unroll
+                    for (int j = 0; j < PG; ++j) acc[h][j] = mma(a, b[j][ks], acc[h][j]);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < PG; ++j) {
+                if (pf[j] < 0) continue;
+                u32x4_t o;
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+#pragma unroll
+                    for (int e = 0; e < 2; ++e)
+                        o[2 * h + e] = H16<T>::pack(apply_act(acc[h][j][2 * e] + bias[ct][h][2 * e], k.act),
+                                                    apply_act(acc[h][j][2 * e + 1] + bias[ct][h][2 * e + 1], k.act));
+                *(u32x4_t*)((T*)k.y + map_frame(k.ym, pf[j]) * k.y_is + (long long)prr[j] * k.y_ld + k.y_c0 + ct * 32 +
+                            8 * g) = o;
+            }
+        }
+    }
+}
+
+bool use_pointwise(const dbsr_conv_desc* d) {
+    return is16(d->x.dtype) && d->y.dtype == d->x.dtype && !d->precise && d->out_mode == DBSR_OUT_NHWC &&
+           !d->res.ptr && !d->gate.ptr && d->kh == 1 && d->kw == 1 && d->stride == 1 && d->pad == 0 &&
+           d->cin % 32 == 0 && d->cin <= 512 && ((d->cin / 32) & (d->cin / 32 - 1)) == 0 && (d->cout == 32 || d->cout == 64) && d->cout * d->cin <= 32768 &&
+           d->y.ld % 8 == 0 && d->y.c0 % 8 == 0 && g_tiled_enabled &&
+           (long long)d->n_frames * d->out_h * d->out_w >= 4096;
+}
+
+template <typename T, int CT, int PG, int NW>
+int launch_pointwise_cfg(const ConvK& k, hipStream_t s) {
+    const int ngroups = (k.npix + PG * 16 - 1) / (PG * 16);
+    const int ks = k.Kp / 32;
+    const int lds = CT * 32 * k.Kp * 2;                 // bytes of the block's weight copy
+    const unsigned grid = (unsigned)std::min((ngroups + NW - 1) / NW, 256 * (lds <= 40960 ? 3 : 2));
+#define DBSR_PW(KS) \
+    if (ks == KS) { hipLaunchKernelGGL((conv1x1_kernel<T, CT, KS, PG, NW>), dim3(grid), dim3(NW * 64), 0, s, k, ngroups); }
+    DBSR_PW(1) DBSR_PW(2) DBSR_PW(4) DBSR_PW(8) DBSR_PW(16)
+#undef DBSR_PW
+    DBSR_CHECK_ARG(ks == 1 || ks == 2 || ks == 4 || ks == 8 || ks == 16, "conv1x1: cin %d not 32/64/128/256/512", k.Kp);
+    DBSR_LAUNCH_CHECK();
+    return 0;
+}
+
+template <typename T, int CT>
+int launch_pointwise_ct(const ConvK& k, hipStream_t s) {
+    // 16-pixel groups, 8 waves, 4 waves per SIMD: proj_oth 55 us (32-pixel groups at 2 waves per SIMD,
+    // 4 or 8 waves per block: 57-59 us)
+    return launch_pointwise_cfg<T, CT, 1, 8>(k, s);
+}
+
+template <typename T>
+int launch_pointwise(const ConvK& k, hipStream_t s) {
+    return k.cout == 64 ? launch_pointwise_ct<T, 2>(k, s) : launch_pointwise_ct<T, 1>(k, s);
+}
+
 ConvK make_convk(const dbsr_conv_desc* d) {
     ConvK k;
     k.x = d->x.ptr; k.x_is = d->x.img_stride; k.x_ld = d->x.ld; k.xm = d->x.map; k.in_h = d->in_h; k.in_w = d->in_w;
@@ -1762,6 +1881,7 @@ extern "C" int dbsr_conv_kernel_for(const dbsr_conv_desc* d) {
     if (pick_ws(d)) return 4;
     if (pick_pipe(d)) return 2;
     if (use_upsample(d, make_convk(d))) return 3;
+    if (use_pointwise(d)) return 5;
     return use_tiled(d) ? 1 : 0;
 }
 
@@ -1771,7 +1891,9 @@ extern "C" int dbsr_conv_head_ok(const dbsr_conv_desc* d) {
 }
 
 extern "C" size_t dbsr_conv_workspace_bytes(const dbsr_conv_desc* d) {
-    if (!d || pick_ws(d) || pick_pipe(d) || use_tiled(d) || d->precise || use_upsample(d, make_convk(d))) return 0;
+    if (!d || pick_ws(d) || pick_pipe(d) || use_tiled(d) || d->precise || use_upsample(d, make_convk(d)) ||
+        use_pointwise(d))
+        return 0;
     const ConvK k = make_convk(d);
     int m, n;
     pick_generic_tile(k, m, n);
@@ -1867,6 +1989,7 @@ extern "C" int dbsr_conv2d(const dbsr_conv_desc* d, void* stream) {
         return launch_conv<float, 1, 1, bf16_t>(k, s);
     }
     if (use_upsample(d, k)) return d->x.dtype == DBSR_F16 ? launch_upsample<f16_t>(k, s) : launch_upsample<bf16_t>(k, s);
+    if (use_pointwise(d)) return d->x.dtype == DBSR_F16 ? launch_pointwise<f16_t>(k, s) : launch_pointwise<bf16_t>(k, s);
     if (d->x.dtype == DBSR_F16) return dispatch_conv<f16_t>(k, d, s);
     return d->x.dtype == DBSR_BF16 ? dispatch_conv<bf16_t>(k, d, s) : dispatch_conv<float>(k, d, s);
 }

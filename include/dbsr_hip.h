@@ -108,8 +108,10 @@ int dbsr_conv2d(const dbsr_conv_desc* d, void* stream);
  * generic implicit-GEMM kernel; 1 = no pipelined kernel; 0 = generic kernel only; 3 = as 2 but the
  * pipelined kernel at any tile count (tests). */
 int dbsr_set_conv_algo(int algo);
-/* Which kernel dbsr_conv2d would launch for `d` under the current selection: 3 PixelShuffle upsampler
- * (bf16 1x1 with DBSR_OUT_SHUFFLE, 32 channels per sub-pixel), 2 pipelined, 1 LDS-tiled, 0 generic. */
+/* Which kernel dbsr_conv2d would launch for `d` under the current selection: 5 pointwise projection
+ * (16-bit 1x1, cin 32..512 a power of two, cout 32 | 64, no residual: merging.py:34), 4 weight-stationary,
+ * 3 PixelShuffle upsampler (bf16 1x1 with DBSR_OUT_SHUFFLE, 32 channels per sub-pixel), 2 pipelined,
+ * 1 LDS-tiled, 0 generic. */
 int dbsr_conv_kernel_for(const dbsr_conv_desc* d);
 /* A 32-channel ResBlock conv2 fused with a 1x1 head (the decoder's last post-ResBlock + RGB predictor,
  * decoders.py:59-61 / blocks.py:94-96): t = ReLU(conv(x) + bias + residual) stays in registers (d->y is

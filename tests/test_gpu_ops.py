@@ -260,6 +260,37 @@ def test_conv1x1_pixelshuffle(ops, case):
     np.testing.assert_array_equal(outs[2].numpy(), outs[0].numpy())
 
 
+@pytest.mark.parametrize('case', [(2, 512, 64, 48, 48, torch.bfloat16, 1, True),    # merge projection shape
+                                  (3, 512, 64, 37, 41, torch.float16, 1, True),     # ragged pixel count
+                                  (5, 128, 32, 29, 33, torch.bfloat16, 0, False),   # 32 couts, no bias/act
+                                  (1, 256, 64, 64, 64, torch.bfloat16, 1, True)])
+def test_conv1x1_pointwise(ops, case):
+    """Pointwise projection kernel (merging.py:34 feat_project_layer, dbsr_conv_kernel_for == 5) against
+    torch on the same 16-bit operands and against the generic kernel (algo 0)."""
+    from dbsr_amd import _lib
+    N, Cin, Cout, H, W, dt, act, with_bias = case
+    gen = torch.Generator().manual_seed(Cin + Cout + H * W)
+    x = torch.randn(N, Cin, H, W, generator=gen)
+    w = torch.randn(Cout, Cin, 1, 1, generator=gen) / Cin ** 0.5
+    b = torch.randn(Cout, generator=gen) * 0.1 if with_bias else None
+    xb, wb = x.to(dt).float(), w.to(dt).float()
+    ref = F.conv2d(xb, wb, b)
+    if act:
+        ref = F.relu(ref)
+    outs = {}
+    try:
+        for algo in (2, 0):
+            _lib.lib().dbsr_set_conv_algo(algo)
+            outs[algo] = ops.conv2d(x.to(DEV), w.to(DEV), b.to(DEV) if b is not None else None, act=act,
+                                    compute_dtype=dt).float().cpu()
+            if algo == 2:
+                assert ops.conv2d.last_kernel == 5
+    finally:
+        _lib.lib().dbsr_set_conv_algo(2)
+    np.testing.assert_allclose(outs[2].numpy(), ref.numpy(), atol=2e-2, rtol=1e-2)
+    np.testing.assert_allclose(outs[2].numpy(), outs[0].numpy(), atol=1e-2, rtol=8e-3)
+
+
 @pytest.mark.parametrize('shape', [(2, 32, 384, 384), (1, 16, 13, 21), (3, 8, 9, 4)])
 def test_gauss_blur3(shape):
     """Sliding-window 3x3 Gaussian (upsampling.py:59-65, filtering.py:29-40) against the oracle's blur."""
