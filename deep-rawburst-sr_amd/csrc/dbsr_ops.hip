@@ -608,6 +608,52 @@ __global__ __launch_bounds__(256) void blur3_kernel(int n, int h, int w, int gro
     }
 }
 
+// 16-bit variant: every row load of the strip (ROWS + 2 rows x 3 columns, raw 16-B, 120 VGPRs at 8 rows)
+// is issued before the first FMA, so a thread waits one memory latency instead of one per row.
+template <typename T, int ROWS>
+__global__ __launch_bounds__(256) void blur3_h16_kernel(int n, int h, int w, int groups, dbsr_tensor in, K9 kk,
+                                                        dbsr_tensor out) {
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int strips = (h + ROWS - 1) / ROWS;
+    if (idx >= (long long)n * strips * w * groups) return;
+    const int g = (int)(idx % groups);
+    long long r = idx / groups;
+    const int x = (int)(r % w);
+    r /= w;
+    const int st = (int)(r % strips);
+    const int f = (int)(r / strips);
+    const T* base = img_ptr<T>(in, f) + g * 8;
+    T* obase = img_ptr<T>(out, f) + g * 8;
+    const int y0 = st * ROWS;
+    u32x4_t raw[ROWS + 2][3];
+#pragma unroll
+    for (int i = 0; i < ROWS + 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int yy = y0 + i - 1, xx = x + j - 1;
+            raw[i][j] = u32x4_t{0u, 0u, 0u, 0u};
+            if ((unsigned)yy < (unsigned)h && (unsigned)xx < (unsigned)w)
+                raw[i][j] = *(const u32x4_t*)(base + ((long long)yy * w + xx) * in.ld);
+        }
+#pragma unroll
+    for (int t = 0; t < ROWS; ++t) {
+        const int y = y0 + t;
+        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const float kv = kk.k[i * 3 + j];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    acc[2 * q] = fmaf(kv, H16<T>::lo(raw[t + i][j][q]), acc[2 * q]);
+                    acc[2 * q + 1] = fmaf(kv, H16<T>::hi(raw[t + i][j][q]), acc[2 * q + 1]);
+                }
+            }
+        if (y < h) store8(obase + ((long long)y * w + x) * out.ld, acc);
+    }
+}
+
 inline unsigned nblocks(long long total, int bs) { return (unsigned)((total + bs - 1) / bs); }
 bool map_ok(const dbsr_tensor& t) { return t.ptr && t.map.fpg > 0; }
 bool vec_ok(const dbsr_tensor& t, int v) { return t.ld % v == 0 && t.c0 % v == 0; }
@@ -774,8 +820,13 @@ extern "C" int dbsr_gauss_blur3(int n, int h, int w, int c, dbsr_tensor in, cons
     const long long total = (long long)n * ((h + BLUR_ROWS - 1) / BLUR_ROWS) * w * (c / 8);
     return by_dtype(in.dtype, [&](auto* tag) {
         using T = std::remove_pointer_t<decltype(tag)>;
-        hipLaunchKernelGGL(blur3_kernel<T>, dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, n, h, w,
-                           c / 8, in, kk, out);
+        // 16-bit: load-first strips of 8 rows (dec.blur 38.0 -> 31.4 us; strips of 4 rows: 32.5 us)
+        if constexpr (sizeof(T) == 2) {
+            hipLaunchKernelGGL((blur3_h16_kernel<T, BLUR_ROWS>), dim3(nblocks(total, 256)), dim3(256), 0,
+                               (hipStream_t)stream, n, h, w, c / 8, in, kk, out);
+        } else
+            hipLaunchKernelGGL(blur3_kernel<T>, dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, n, h,
+                               w, c / 8, in, kk, out);
         DBSR_LAUNCH_CHECK();
         return 0;
     });

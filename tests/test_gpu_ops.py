@@ -291,18 +291,23 @@ def test_conv1x1_pointwise(ops, case):
     np.testing.assert_allclose(outs[2].numpy(), outs[0].numpy(), atol=1e-2, rtol=8e-3)
 
 
+@pytest.mark.parametrize('dt', [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize('shape', [(2, 32, 384, 384), (1, 16, 13, 21), (3, 8, 9, 4)])
-def test_gauss_blur3(shape):
-    """Sliding-window 3x3 Gaussian (upsampling.py:59-65, filtering.py:29-40) against the oracle's blur."""
+def test_gauss_blur3(shape, dt):
+    """Sliding-window 3x3 Gaussian (upsampling.py:59-65, filtering.py:29-40) against the oracle's blur
+    (16-bit: on the rounded input, fp32 sums, one rounding of the output)."""
     from dbsr_amd import _lib as L
     N, C, H, W = shape
-    x = torch.randn(N, C, H, W, generator=torch.Generator().manual_seed(H + W + C))
+    x = torch.randn(N, C, H, W, generator=torch.Generator().manual_seed(H + W + C)).to(dt).float()
     kern = orc.gauss_kernel(3, 1.0).reshape(3, 3).float()
     ref = F.conv2d(x, kern.expand(C, 1, 3, 3).contiguous(), padding=1, groups=C)
-    xs = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+    if dt != torch.float32:
+        ref = ref.to(dt).float()
+    xs = x.permute(0, 2, 3, 1).contiguous().to(dt).to(DEV)
     out = torch.zeros_like(xs)
     import ctypes
     kb = (ctypes.c_float * 9)(*kern.flatten().tolist())
     L.check(L.lib().dbsr_gauss_blur3(N, H, W, C, L.tensor_desc(xs, C), kb, L.tensor_desc(out, C),
                                      L.stream_ptr(xs.device)), 'blur')
-    np.testing.assert_allclose(out.permute(0, 3, 1, 2).cpu().numpy(), ref.numpy(), atol=1e-5, rtol=1e-5)
+    tol = 1e-5 if dt == torch.float32 else (2 ** -8 if dt == torch.bfloat16 else 2 ** -11)
+    np.testing.assert_allclose(out.permute(0, 3, 1, 2).float().cpu().numpy(), ref.numpy(), atol=1e-5, rtol=tol)
