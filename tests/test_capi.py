@@ -61,6 +61,35 @@ def test_splitk_workspace_query(L):
     assert L.lib().dbsr_conv_workspace_bytes(d) == 0
 
 
+def test_pointwise_dispatch(L):
+    """dbsr_conv_kernel_for (host logic only): the merge's 1x1 512->64 projection over 104 frames takes the
+    pointwise kernel (5); fp32, a residual, a non-power-of-two cin or a tiny pixel count do not."""
+    lib = L.lib()
+    d = L.ConvDesc()
+    d.n_frames = 104
+    d.x = L.Tensor(1, L.DBSR_BF16, 48 * 48 * 512, 512, 0, L.FrameMap(1, 1, 0, 1))
+    d.in_h = d.in_w = d.out_h = d.out_w = 48
+    d.cin, d.cout, d.kh, d.kw, d.stride, d.pad, d.dil = 512, 64, 1, 1, 1, 0, 1
+    d.w = 1
+    d.y = L.Tensor(1, L.DBSR_BF16, 48 * 48 * 192, 192, 0, L.FrameMap(13, 14, 1, 1))
+    d.res = L.NULL_TENSOR
+    assert lib.dbsr_conv_kernel_for(d) == 5
+    assert lib.dbsr_conv_workspace_bytes(d) == 0
+    d.cout = 32
+    assert lib.dbsr_conv_kernel_for(d) == 5
+    d.cin = 96
+    assert lib.dbsr_conv_kernel_for(d) != 5
+    d.cin = 512
+    d.n_frames, d.in_h, d.in_w, d.out_h, d.out_w = 1, 8, 8, 8, 8          # 64 pixels: generic kernel
+    assert lib.dbsr_conv_kernel_for(d) != 5
+    d.n_frames, d.in_h, d.in_w, d.out_h, d.out_w = 104, 48, 48, 48, 48
+    d.res = L.Tensor(1, L.DBSR_BF16, 48 * 48 * 32, 32, 0, L.FrameMap(1, 1, 0, 1))
+    assert lib.dbsr_conv_kernel_for(d) != 5
+    d.res = L.NULL_TENSOR
+    d.x.dtype = d.y.dtype = L.DBSR_F32
+    assert lib.dbsr_conv_kernel_for(d) != 5
+
+
 def test_packed_size(L):
     # cin 117 -> 128 (cin > 16 pads to 32: 16 groups of 8) * 9 taps = 144 k-groups; cout 128 -> 128 rows;
     # 3x3 with cin > 16: followed by the chunk-major copy of the pipelined kernel (same size)
