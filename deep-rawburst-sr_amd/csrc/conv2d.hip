@@ -1510,7 +1510,7 @@ size_t splitk_bytes(const ConvK& k, int sp) {
 // (a few hundred pixels) fall through to 16 x 64-pixel tiles (and split-K) for parallelism
 void pick_generic_tile(const ConvK& k, int& best_m, int& best_n) {
     const int mts[3] = {4, 2, 1}, nts[3] = {4, 2, 1};
-    const long long minb = 512;
+    const long long minb = 512;   // 1024 / 2048 / 4096 measured: enc.init 21.4 / 25.7 / 29.3 us vs 23.1
     best_m = 1;
     best_n = 1;
     for (int a = 0; a < 3; ++a) {
