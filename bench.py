@@ -2,10 +2,17 @@
 SyntheticBurstVal-shaped 14x48x48 RAW bursts -> 384x384 RGB, configs[1]: bf16, batch 8 per GPU).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 8] [--frames 14] [--size 48]
-                  [--dtype bf16|fp32] [--no-graph] [--no-cpu-baseline]
+                  [--dtype fp16|bf16|fp32] [--no-graph] [--no-cpu-baseline]
 
-One process per GPU (torchrun for N>1); every rank runs its own batch of independent bursts (the
-path shards over bursts with no data-path collective: weak scaling).  A step = one full forward
+One process per GPU.  Under torchrun (WORLD_SIZE set) this process is one rank; with --gpus N > 1 and no
+WORLD_SIZE, bench.py itself starts the N ranks (torch.distributed.run, before anything touches the GPU)
+and exits with their status.  Every rank runs its own shard of the global batch (N x --batch independent
+bursts; the path shards over bursts with no data-path collective: weak scaling).
+
+Storage dtype: fp16 by default.  bf16 (configs[1]'s text) misses the metric's "PSNR within 0.01 dB" bar:
+0.01 dB at the reference's published 39.17 dB is an RMS prediction error of 5.3e-4, and bf16 storage gives
+~2.9e-3 against the fp32 oracle, fp16 ~4e-4 (tests/test_gpu_parity.py, DESIGN.md "Precision").  fp16 and
+bf16 run at the same dense MFMA rate (2.5 PF) and move the same bytes.  A step = one full forward
 (PWC-Net alignment, encoder, warp, merging/fusion incl. the fusion_weights aux output, decoder) over
 one batch of synthetic bursts already resident in HBM, replayed as one HIP graph.  Timing: W untimed
 steps, then K steps bracketed by barrier + synchronize, max over ranks.  Rank 0 prints one JSON line.
@@ -14,6 +21,8 @@ import argparse
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -23,7 +32,22 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
-PEAK_MFMA_TFLOPS = {'bf16': 2500.0, 'fp32': 157.3}    # dense peaks (MI355X_MICROARCH.md chip table)
+PEAK_MFMA_TFLOPS = {'bf16': 2500.0, 'fp16': 2500.0, 'fp32': 157.3}   # dense peaks (MI355X_MICROARCH.md chip table)
+DTYPES = {'bf16': 'bfloat16', 'fp16': 'float16', 'fp32': 'float32'}
+# conv-like kernel families (MFMA-bound; bench reports each against the dense peak)
+CONV_FAMILIES = ('conv3x3_ws', 'conv3x3_pipe', 'conv3x3_tiled', 'conv2d_generic', 'conv1x1', 'conv1x1_shuffle',
+                 'conv_fuse', 'pwc_dense')
+KERNEL_DESC = {'conv3x3_ws': 'conv3x3_ws_kernel (persistent weight-stationary implicit-GEMM 3x3, Cin <= 64',
+               'conv3x3_pipe': 'conv3x3_pipe_kernel (persistent LDS-DMA-pipelined implicit-GEMM 3x3',
+               'conv3x3_tiled': 'conv3x3_tiled_kernel (LDS-tiled implicit-GEMM 3x3',
+               'conv2d_generic': 'conv2d_kernel (generic implicit-GEMM',
+               'conv1x1': 'conv1x1_kernel (pointwise projection, LDS-resident weights',
+               'conv1x1_shuffle': 'upsample_shuffle_kernel (1x1 conv + PixelShuffle',
+               'conv_fuse': 'conv_fuse_kernel (weight-predictor output conv + softmax + fusion',
+               'pwc_dense': 'pwc_dense_kernel (PWC-Net DenseNet decoder level in one launch'}
+# PMC traffic per launch of each kernel family, from the committed rocprofv3 --pmc passes of this same
+# command (tools/profile.sh -> tools/summarize_profile.py); bench.py cannot read its own counters
+TRAFFIC_FILE = os.path.join(REPO, 'profiles', 'pmc_traffic.json')
 
 
 def parse():
@@ -34,7 +58,8 @@ def parse():
     ap.add_argument('--batch', type=int, default=8)
     ap.add_argument('--frames', type=int, default=14)
     ap.add_argument('--size', type=int, default=48)
-    ap.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
+    ap.add_argument('--dtype', default=None, choices=['fp16', 'bf16', 'fp32'],
+                    help='storage dtype (default fp16 for --mode infer, bf16 for --mode train)')
     ap.add_argument('--no-graph', action='store_true')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
@@ -42,7 +67,61 @@ def parse():
     ap.add_argument('--zero-flow', action='store_true', help='diagnostic: identity-flow stub instead of PWC-Net')
     ap.add_argument('--mode', default='infer', choices=['infer', 'train'],
                     help='train: configs[3] training step (defaults 128x128, batch 8 per GPU, RCCL grad all-reduce)')
+    ap.add_argument('--dry-run', action='store_true',
+                    help='CPU check of the rank launcher: gloo, no GPU; rank 0 prints every rank\'s batch shard')
     return ap.parse_args()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n):
+    """--gpus n > 1 outside torchrun: run this same command as n ranks of one node (torch.distributed.run,
+    rendezvous on 127.0.0.1) as a CHILD process -- this process has not touched the GPU and never execs --
+    and return the launcher's exit status (admin/multigpu.py:8-14 is the reference's single-process
+    nn.DataParallel; here it is one process per GPU)."""
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={n}',
+           '--master-addr=127.0.0.1', f'--master-port={_free_port()}', os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def cpu_model():
+    try:
+        for line in open('/proc/cpuinfo'):
+            if line.startswith('model name'):
+                return line.split(':', 1)[1].strip()
+    except OSError:
+        pass
+    return 'unknown'
+
+
+def load_traffic():
+    try:
+        return json.load(open(TRAFFIC_FILE))
+    except (OSError, ValueError):
+        return {}
+
+
+def dry_run(args, world, rank):
+    """The launcher's rank layout without a GPU: every rank derives its shard of the global batch exactly as
+    the GPU path does, and rank 0 all-gathers and prints them."""
+    import torch.distributed as td
+    from dbsr_amd.parallel import shard_range
+    td.init_process_group('gloo')
+    gb = args.batch * world
+    lo, hi = shard_range(gb, rank, world)
+    t = torch.tensor([rank, world, lo, hi], dtype=torch.int64)
+    got = [torch.zeros_like(t) for _ in range(world)]
+    td.all_gather(got, t)
+    if rank == 0:
+        print(json.dumps({'dry_run': True, 'n_gpus': world, 'global_batch': gb,
+                          'ranks': [g.tolist() for g in got]}))
+    td.destroy_process_group()
 
 
 def train_main(args, world, rank, dev, dist):
@@ -52,7 +131,7 @@ def train_main(args, world, rank, dev, dist):
     from dbsr_amd.burst import synthetic_bursts
     from dbsr_amd.training import DBSRTrainer
     B, N, S = args.batch, args.frames, (args.size if args.size != 48 else 128)
-    dtype = torch.bfloat16 if args.dtype == 'bf16' else torch.float32
+    dtype = getattr(torch, DTYPES[args.dtype])
     net = dbsr_amd.build_synthetic_net(seed=0).to(dev).set_compute_dtype(dtype)
     tr = DBSRTrainer(net)
     burst, gt = synthetic_bursts(B, N, S, S, sr_factor=8, seed=2000 + rank)
@@ -106,14 +185,23 @@ def cpu_baseline(N, H, W, seconds):
             if el >= seconds or n >= 50:
                 break
     return {'value': n / el, 'unit': 'bursts/s', 'cores': torch.get_num_threads(), 'kind': 'port',
+            'cpu_model': cpu_model(), 'host_cpus': os.cpu_count(),
             'sample': f'{n} batch-1 bursts of {N}x{H}x{W} (fp32 oracle/dbsr_oracle.py, {el:.1f} s)'}
 
 
 def main():
     args = parse()
+    if args.dtype is None:
+        args.dtype = 'bf16' if args.mode == 'train' else 'fp16'
+    if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world != args.gpus:
+        raise SystemExit(f'bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: one rank per GPU')
+    if args.dry_run:
+        return dry_run(args, world, rank)
     dist = world > 1
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
@@ -128,13 +216,16 @@ def main():
         return
     import dbsr_amd
     from dbsr_amd.burst import synthetic_bursts
-    dtype = torch.bfloat16 if args.dtype == 'bf16' else torch.float32
+    from dbsr_amd.parallel import shard_range
+    dtype = getattr(torch, DTYPES[args.dtype])
     net = dbsr_amd.build_synthetic_net(seed=0).to(dev).eval()
     net.set_compute_dtype(dtype)
     net.use_graph = not args.no_graph
     net.zero_flow = args.zero_flow
     B, N, S = args.batch, args.frames, args.size
-    burst, _ = synthetic_bursts(B, N, S, S, sr_factor=8, seed=1000 + rank)
+    lo, hi = shard_range(B * world, rank, world)     # this rank's bursts [lo, hi) of the global batch
+    assert hi - lo == B
+    burst, _ = synthetic_bursts(B, N, S, S, sr_factor=8, seed=1000 + lo)
     burst = burst.to(dev)
 
     with torch.no_grad():
@@ -170,45 +261,41 @@ def main():
         f[0] += ms
         f[1] += plan.work[i][1] if i in plan.work else 0.0
         f[2] += 1
-    conv_flop = sum(w for kind, (ms, w, n) in fam.items() if kind.startswith('conv'))
+    is_conv = lambda k: k in CONV_FAMILIES                  # noqa: E731
+    conv_flop = sum(w for kind, (ms, w, n) in fam.items() if is_conv(kind))
     peak_t = PEAK_MFMA_TFLOPS[args.dtype]
+    traffic = load_traffic() if args.dtype != 'fp32' else {}
     # the dominant kernel family (most device time per forward)
-    dom = max((k for k in fam if k.startswith('conv')), key=lambda k: fam[k][0])
+    dom = max((k for k in fam if is_conv(k)), key=lambda k: fam[k][0])
     t_ms, t_flop, t_n = fam[dom]
     t_tf = t_flop / (t_ms * 1e-3) / 1e12
-    kdesc = {'conv3x3_ws': 'conv3x3_ws_kernel (persistent weight-stationary implicit-GEMM 3x3, Cin <= 64',
-             'conv3x3_pipe': 'conv3x3_pipe_kernel (persistent LDS-DMA-pipelined implicit-GEMM 3x3',
-             'conv3x3_tiled': 'conv3x3_tiled_kernel (LDS-tiled implicit-GEMM 3x3',
-             'conv2d_generic': 'conv2d_kernel (generic implicit-GEMM',
-             'conv1x1': 'conv1x1_kernel (pointwise projection, LDS-resident weights',
-             'conv1x1_shuffle': 'upsample_shuffle_kernel (1x1 conv + PixelShuffle',
-             'conv_fuse': 'conv_fuse_kernel (weight-predictor output conv + softmax + fusion'}[dom]
-    roof = {'bound': 'mfma', 'kernel': kdesc + ', %d launches per forward; '
-                                       'achieved = their algorithmic FLOPs / their summed event-timed durations)' % t_n,
+    roof = {'bound': 'mfma', 'kernel': KERNEL_DESC[dom] + ', %d launches per forward; achieved = their algorithmic '
+                                                         'FLOPs / their summed event-timed durations)' % t_n,
             'achieved': round(t_tf, 2), 'peak': peak_t, 'unit': 'TFLOP/s', 'frac': round(t_tf / peak_t, 4),
-            'traffic': None}
+            'traffic': traffic.get(dom, {}).get('bytes_per_launch'),
+            'traffic_source': traffic.get(dom, {}).get('source')}
     # every conv family against the same dense peak (the roofline object above is the dominant one)
     fam_roof = {k: {'achieved_tflops': round(w / (ms * 1e-3) / 1e12, 2), 'frac': round(w / (ms * 1e-3) / 1e12 / peak_t, 4),
-                    'ms': round(ms, 4), 'launches': n}
-                for k, (ms, w, n) in fam.items() if k.startswith('conv') and ms > 0}
-    conv_ms = sum(ms for kind, (ms, w, n) in fam.items() if kind.startswith('conv'))
-    conv_n = sum(n for kind, (ms, w, n) in fam.items() if kind.startswith('conv'))
+                    'ms': round(ms, 4), 'launches': n, 'traffic': traffic.get(k, {}).get('bytes_per_launch')}
+                for k, (ms, w, n) in fam.items() if is_conv(k) and ms > 0}
+    conv_ms = sum(ms for kind, (ms, w, n) in fam.items() if is_conv(kind))
+    conv_n = sum(n for kind, (ms, w, n) in fam.items() if is_conv(kind))
     all_conv_tf = conv_flop / (conv_ms * 1e-3) / 1e12
     hbm = {}
     for k in ('warp', 'fuse'):
         if k in fam:
-            ms, by, _ = fam[k]
+            ms, by, n = fam[k]
             gbs = by / (ms * 1e-3) / 1e9
             hbm[k] = {'bound': 'hbm', 'achieved': round(gbs, 1), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
-                      'frac': round(gbs / PEAK_HBM_GBS, 4), 'traffic': None, 'us': round(ms * 1e3, 2),
-                      'alg_bytes': by}
+                      'frac': round(gbs / PEAK_HBM_GBS, 4), 'traffic': traffic.get(k, {}).get('bytes_per_launch'),
+                      'us': round(ms * 1e3, 2), 'alg_bytes': by / n}
     if args.kernel_breakdown and rank == 0:
         for i, (name, ms) in enumerate(times):
             if name.startswith('sync.'):
                 continue
             kind = plan.kernel.get(i) or '-'
             w = plan.work[i][1] if i in plan.work else 0.0
-            rate = '%8.1f %s' % ((w / (ms * 1e-3) / 1e12, 'TF/s') if kind.startswith('conv') else
+            rate = '%8.1f %s' % ((w / (ms * 1e-3) / 1e12, 'TF/s') if is_conv(kind) else
                                  (w / (ms * 1e-3) / 1e9, 'GB/s')) if (w and ms) else ''
             print(f'{name:32s} {ms * 1e3:9.1f} us  {kind:15s} {rate}', file=sys.stderr)
         for k, (ms, w, n) in sorted(fam.items(), key=lambda kv: -kv[1][0]):
@@ -234,7 +321,7 @@ def main():
             'roofline': roof, 'roofline_hbm': hbm,
             'roofline_families': fam_roof,
             'conv_all': {'achieved_tflops': round(all_conv_tf, 2), 'launches': conv_n,
-                         'ms_by_kernel': {k: round(v[0], 3) for k, v in fam.items() if k.startswith('conv')}},
+                         'ms_by_kernel': {k: round(v[0], 3) for k, v in fam.items() if is_conv(k)}},
             'cpu_baseline': cpu,
             'conv_flop_per_step': conv_flop,
         }

@@ -30,6 +30,11 @@
 #include <algorithm>
 #include <type_traits>
 
+// Measured slower than dbsr_conv2d + dbsr_fuse_softmax and therefore not in the product
+// library: built only with -DDBSR_EXPERIMENTAL=1 (`make exp EXP_FLAGS=-DDBSR_EXPERIMENTAL=1 EXP_NAME=fuse`, then
+// DBSR_HIP_LIB=.../libdbsr_hip_fuse.so).  Without it the two entry points report the shape as unserved.
+#if DBSR_EXPERIMENTAL
+
 using namespace dbsr;
 
 namespace {
@@ -449,3 +454,13 @@ extern "C" int dbsr_conv_fuse_softmax(const dbsr_conv_desc* d, int B, int N, dbs
     DBSR_LAUNCH_CHECK();
     return 0;
 }
+
+#else
+extern "C" int dbsr_conv_fuse_ok(const dbsr_conv_desc*, int, int) { return 0; }
+
+extern "C" int dbsr_conv_fuse_softmax(const dbsr_conv_desc*, int, int, dbsr_tensor, dbsr_tensor, dbsr_tensor,
+                                      dbsr_tensor, void*) {
+    DBSR_CHECK_ARG(false, "conv_fuse_softmax: experimental kernel not built (-DDBSR_EXPERIMENTAL=1)");
+    return 0;
+}
+#endif

@@ -21,7 +21,9 @@
 
 #include <map>
 #include <mutex>
+#include <optional>
 #include <tuple>
+#include <vector>
 
 #include "../../../include/dbsr_hip.h"
 
@@ -184,18 +186,52 @@ std::tuple<at::Tensor, at::Tensor> fuse_backward(const at::Tensor& weights, cons
     return {back(dl), back(df)};
 }
 
-// packed weights per (weight storage, version, dtype): repacking on every call is what made the
-// op-level conv slow; a parameter update bumps the version and repacks once
-struct PackKey {
-    const void* ptr;
-    int64_t version;
-    int dtype;
-    bool operator<(const PackKey& o) const {
-        return std::tie(ptr, version, dtype) < std::tie(o.ptr, o.version, o.dtype);
-    }
+// Packed weights, one cache entry per weight tensor (repacking on every call is what made the op-level conv
+// slow).  An entry is valid only while it describes the same live tensors: weak
+// references to the weight's and the bias's TensorImpl (a freed tensor whose address a new one reuses never
+// matches), their versions (an optimizer step bumps them and repacks once), data pointers, shapes and the
+// compute dtype.  A stale entry is replaced, and entries of freed weights are evicted on every insert, so the
+// cache holds at most one packed copy per live weight.  In-place writes that bypass version counting
+// (`p.data.copy_(...)`, raw pointers) are invisible to it: call torch.ops.dbsr.clear_pack_cache() after them.
+using WeakImpl = c10::weak_intrusive_ptr<c10::TensorImpl, c10::UndefinedTensorImpl>;
+struct PackEntry {
+    std::optional<WeakImpl> w, b;  // b empty when the conv has no bias
+    int64_t w_version = -1, b_version = -1;
+    const void* w_ptr = nullptr;
+    const void* b_ptr = nullptr;
+    std::vector<int64_t> w_shape;
+    int dtype = -1;
+    at::Tensor wp, bp;
 };
 std::mutex g_pack_mu;
-std::map<PackKey, std::pair<at::Tensor, at::Tensor>> g_pack_cache;
+std::map<const c10::TensorImpl*, PackEntry> g_pack_cache;
+
+bool same_live(const std::optional<WeakImpl>& weak, const at::Tensor& t) {
+    if (!weak) return false;
+    auto strong = weak->lock();
+    return strong.defined() && strong.get() == t.unsafeGetTensorImpl();
+}
+
+bool entry_valid(const PackEntry& e, const at::Tensor& w, const c10::optional<at::Tensor>& bias, int dc) {
+    if (!same_live(e.w, w) || e.w_version != (int64_t)w._version() || e.w_ptr != w.data_ptr() ||
+        e.w_shape != w.sizes().vec() || e.dtype != dc)
+        return false;
+    const bool has_b = bias.has_value() && bias->defined();
+    if (has_b != e.bp.defined()) return false;
+    if (has_b && (!same_live(e.b, *bias) || e.b_version != (int64_t)bias->_version() || e.b_ptr != bias->data_ptr()))
+        return false;
+    return true;
+}
+
+void clear_pack_cache() {
+    std::lock_guard<std::mutex> lk(g_pack_mu);
+    g_pack_cache.clear();
+}
+
+int64_t pack_cache_size() {
+    std::lock_guard<std::mutex> lk(g_pack_mu);
+    return (int64_t)g_pack_cache.size();
+}
 
 at::Tensor conv2d_fused(const at::Tensor& x, const at::Tensor& weight, const c10::optional<at::Tensor>& bias,
                         int64_t stride, int64_t padding, int64_t dilation, int64_t act,
@@ -210,23 +246,40 @@ at::Tensor conv2d_fused(const at::Tensor& x, const at::Tensor& weight, const c10
     const int64_t ow = (W + 2 * padding - dilation * (kw - 1) - 1) / stride + 1;
     void* s = cur_stream();
     at::Tensor wp, bp;
+    const bool has_b = bias.has_value() && bias->defined();
+    if (has_b) TORCH_CHECK(bias->dim() == 1 && bias->size(0) == Cout, "dbsr::conv2d_fused: bias must be [Cout]");
     {
         std::lock_guard<std::mutex> lk(g_pack_mu);
-        PackKey key{weight.data_ptr(), weight._version(), dc};
-        auto it = g_pack_cache.find(key);
-        if (it == g_pack_cache.end()) {
-            auto w32 = weight.to(at::kFloat).contiguous();
-            auto b32 = bias.has_value() ? bias->to(at::kFloat).contiguous() : at::Tensor();
-            wp = at::empty({(int64_t)dbsr_conv_packed_elems(Cout, Cin, kh, kw)}, x.options());
-            bp = bias.has_value() ? at::empty({Cout}, x.options().dtype(at::kFloat)) : at::Tensor();
-            check(dbsr_conv_pack_weights(w32.data_ptr<float>(), bias.has_value() ? b32.data_ptr<float>() : nullptr,
-                                         Cout, Cin, kh, kw, dc, 1, wp.data_ptr(),
-                                         bias.has_value() ? bp.data_ptr<float>() : nullptr, s),
-                  "dbsr_conv_pack_weights");
-            g_pack_cache[key] = {wp, bp};
+        auto it = g_pack_cache.find(weight.unsafeGetTensorImpl());
+        if (it != g_pack_cache.end() && entry_valid(it->second, weight, bias, dc)) {
+            wp = it->second.wp;
+            bp = it->second.bp;
         } else {
-            wp = it->second.first;
-            bp = it->second.second;
+            auto w32 = weight.to(at::kFloat).contiguous();
+            auto b32 = has_b ? bias->to(at::kFloat).contiguous() : at::Tensor();
+            wp = at::empty({(int64_t)dbsr_conv_packed_elems(Cout, Cin, kh, kw)}, x.options());
+            bp = has_b ? at::empty({Cout}, x.options().dtype(at::kFloat)) : at::Tensor();
+            check(dbsr_conv_pack_weights(w32.data_ptr<float>(), has_b ? b32.data_ptr<float>() : nullptr,
+                                         Cout, Cin, kh, kw, dc, 1, wp.data_ptr(),
+                                         has_b ? bp.data_ptr<float>() : nullptr, s),
+                  "dbsr_conv_pack_weights");
+            // evict entries whose weight is gone, then (re)place this weight's entry
+            for (auto e = g_pack_cache.begin(); e != g_pack_cache.end();)
+                e = (!e->second.w || e->second.w->expired()) ? g_pack_cache.erase(e) : std::next(e);
+            PackEntry ent;
+            ent.w.emplace(weight.getIntrusivePtr());
+            ent.w_version = weight._version();
+            ent.w_ptr = weight.data_ptr();
+            ent.w_shape = weight.sizes().vec();
+            ent.dtype = dc;
+            if (has_b) {
+                ent.b.emplace(bias->getIntrusivePtr());
+                ent.b_version = bias->_version();
+                ent.b_ptr = bias->data_ptr();
+            }
+            ent.wp = wp;
+            ent.bp = bp;
+            g_pack_cache.insert_or_assign(weight.unsafeGetTensorImpl(), std::move(ent));
         }
     }
     auto xs = nhwc(x, conv_ld(Cin), dt);
@@ -238,7 +291,7 @@ at::Tensor conv2d_fused(const at::Tensor& x, const at::Tensor& weight, const c10
     d.x = desc(xs, conv_ld(Cin));
     d.in_h = H; d.in_w = W; d.cin = Cin;
     d.w = wp.data_ptr();
-    d.bias = bias.has_value() ? bp.data_ptr<float>() : nullptr;
+    d.bias = has_b ? bp.data_ptr<float>() : nullptr;
     d.cout = Cout; d.kh = kh; d.kw = kw; d.stride = stride; d.pad = padding; d.dil = dilation;
     d.y = desc(y, ldy);
     d.out_h = oh; d.out_w = ow;
@@ -275,6 +328,10 @@ TORCH_LIBRARY(dbsr, m) {
     m.def("fuse_backward(Tensor weights, Tensor feats, Tensor fused, Tensor dfused) -> (Tensor, Tensor)");
     m.def("conv2d_fused(Tensor x, Tensor weight, Tensor? bias=None, int stride=1, int padding=0, int dilation=1, "
           "int act=0, Tensor? residual=None, int post_act=0) -> Tensor");
+    m.def("clear_pack_cache() -> ()");
+    m.impl("clear_pack_cache", &clear_pack_cache);
+    m.def("pack_cache_size() -> int");
+    m.impl("pack_cache_size", &pack_cache_size);
 }
 
 // the ROCm build of PyTorch dispatches HIP tensors under the CUDA key

@@ -414,9 +414,6 @@ class PWCPlanner:
 # ==================================================================================================
 class DBSREngine:
     LANE0_CU_SHARE = 0.5      # CU share of lane 0's persistent convs while the PWC lane runs (tools/capbench.sh)
-    PIPELINE_GROUPS = 1       # burst groups (alignment of group g+1 beside merge + decoder of g): 2 measured
-                              # 2037 vs 2388 bursts/s at configs[1] -- the PWC chain is latency-bound, so two
-                              # half-batch chains take twice as long (tools/sweep_engine.py)
     # bf16: fuse the RGB predictor into the last decoder ResBlock conv (False: separate fp32 kernel)
     FUSED_HEAD = True
     # weight-predictor input conv split into a per-frame [proj, offfeat] conv + a per-burst base conv
@@ -433,6 +430,7 @@ class DBSREngine:
         self.device = None
         self.sig = None
         self.plans = {}
+        self.slots = {}
         self.graphs = {}
 
     def matches(self, net):
@@ -487,7 +485,7 @@ class DBSREngine:
                        if pm.bias is not None else None)
         self.device = device
         self.sig = _param_signature(net)
-        self.plans, self.graphs = {}, {}
+        self.plans, self.slots, self.graphs = {}, {}, {}
 
     def _resblocks(self, plan, name, blocks, n, hw, bufs, x_idx, dtype, head=None):
         """ResBlock chain (blocks.py:81-96) over ping-pong buffers; returns index of the result buffer
@@ -502,21 +500,6 @@ class DBSREngine:
             fused = d.fused_head
             a = c
         return (a, fused) if head is not None else a
-
-    def _groups(self, B, mode):
-        """Burst groups of the software pipeline: the alignment chain of group g+1 (PWC-Net + offset-feature
-        extractor: many small latency-bound launches) runs on the side lane while lane 0 runs the merge +
-        decoder of group g.  One group for mode 'partial' and for B == 1."""
-        G = min(B, DBSREngine.PIPELINE_GROUPS) if mode == 'full' else 1
-        bounds = [(i * B) // G for i in range(G + 1)]
-        return [(bounds[i], bounds[i + 1]) for i in range(G)]
-
-    def _emit_align(self, plan, grp, N, H, W, sh):
-        """PWC-Net flow of the group's pairs -> offsets / offset features (flow_finalize) -> offset-feature
-        extractor (merging.py:85-87) -> WP[..., oc:] of the group."""
-        WP = self._emit_flow(plan, grp, N, H, W, sh)
-        self._emit_ofe(plan, grp, N, H, W, sh, WP)
-        return WP
 
     def _emit_flow(self, plan, grp, N, H, W, sh):
         """PWC-Net flow of the group's pairs -> offsets and the offset-feature input (flow_finalize); returns
@@ -649,10 +632,10 @@ class DBSREngine:
         the weight predictor and emit dbsr_fuse_partial statistics of frames [first_frame, N) into
         bufs['stats'] instead of the fusion and the decoder (those run in `_build_combine`).
 
-        Lanes: the alignment chain of a burst group (PWC-Net, flow finalize, offset-feature extractor)
-        runs on side lane 1; lane 0 runs the encoder over the whole batch, then per group waits for that
-        group's alignment and runs its merge + fusion + decoder while lane 1 already aligns the next group
-        (`_groups`).  Single-stream mode issues the same launches in the same order on one stream."""
+        Lanes: PWC-Net and the flow finalize run on side lane 1 while lane 0 runs the encoder, the reference
+        frames' projections and the base term; after the flow join, the offset-feature extractor runs on lane 1
+        beside the warp and the other frames' projections on lane 0; then merge + fusion + decoder on lane 0.
+        Single-stream mode issues the same launches in the same order on one stream."""
         dt, dev = self.dtype, self.device
         lib = L.lib()
         plan = Plan()
@@ -669,18 +652,14 @@ class DBSREngine:
         E = NHWC(F, H, W, C, dt, dev)
         PJ = NHWC(F, H, W, r8(self.proj.cout), dt, dev) if self.wp_split is None else None
         sh = {'rgb': rgb, 'offsets': bufs['offsets'], 'om': om, 'E': E, 'PJ': PJ, 'Hp': Hp, 'Wp': Wp}
-        groups = self._groups(B, mode)
+        grp = (0, B)
         plan.add('pack_burst', lib.dbsr_pack_burst, B, N, H, W, bufs['burst'].data_ptr(), raw.d(0), Hp, Wp,
                  rgb.d(0) if not self.zero_flow else L.NULL_TENSOR)
         # lane-0 persistent convs issued while the side lane runs leave part of the CUs to it
         plan_cap = int(torch.cuda.get_device_properties(dev).multi_processor_count * DBSREngine.LANE0_CU_SHARE) \
             if Plan.MULTI_STREAM else 0
         plan.fork(1, dev, priority=-1)
-        # one burst group: the offset-feature extractor waits on lane 1 until lane 0 has joined the flow, so it
-        # runs beside the warp + projections instead of before them
-        split_ofe = len(groups) == 1
-        WPs = [self._emit_flow(plan, groups[0], N, H, W, sh) if split_ofe else
-               self._emit_align(plan, groups[0], N, H, W, sh)]
+        WP = self._emit_flow(plan, grp, N, H, W, sh)          # PWC-Net on lane 1
         plan.switch(0)
         plan.max_blocks = plan_cap
         # ---------------- encoder (encoders.py:66-72), whole batch ----------------
@@ -697,49 +676,37 @@ class DBSREngine:
             bufs['pred'] = torch.zeros(B, 3, H * self.s, W * self.s, dtype=torch.float32, device=dev)
         plan.fuse_ops = []
         es = 4 if dt == torch.float32 else 2
-        # the first group's base term needs only the encoder: lane 0 computes it before waiting for PWC-Net
-        # (its projections write WP channels [0, pd); the side lane writes the offset features at [pd, ..))
-        BS0 = self._emit_base(plan, groups[0], N, H, W, sh, WPs[0]) if self.wp_split is not None else None
-        for gi, grp in enumerate(groups):
-            plan.join(1)                      # lane 0 waits for this group's alignment chain
-            if gi + 1 < len(groups):
-                plan.switch(1)                # ... while lane 1 aligns the next group
-                WPs.append(self._emit_align(plan, groups[gi + 1], N, H, W, sh))
-                plan.switch(0)
-                plan.max_blocks = plan_cap
-            else:
-                plan.max_blocks = 0
-            Wf = None
-            if split_ofe:
-                plan.switch(1)                # offsets are in: offset features on lane 1 ...
-                self._emit_ofe(plan, grp, N, H, W, sh, WPs[gi])
-                plan.switch(0)
-                Wf = self._emit_warp(plan, grp, N, H, W, sh, WPs[gi])   # ... beside the warp + projections
-                plan.join(1)
-            h, Wf = self._emit_merge(plan, grp, N, H, W, sh, WPs[gi], BS=BS0 if gi == 0 else None, Wf=Wf)
-            g0, g1 = grp
-            Bg = g1 - g0
-            if mode == 'partial':
-                LG = self._emit_logits(plan, Bg * N, H, W, h)
-                ST = torch.zeros(B, H, W, 3 * C, dtype=torch.float32, device=dev)
-                plan.add('merge.fuse_partial', lib.dbsr_fuse_partial, B, N, H * W, C, first_frame, LG.d(0),
-                         E.d(0, (1, N, 0, 1)), Wf.d(0), ST.data_ptr())
-                bufs['stats'] = ST
-                break
-            FUS = NHWC(Bg, H, W, C, dt, dev)
-            fmap = (1, 1, g0 * N, 0)
-            feats = [E.d(0, (1, N, g0 * N, 1)), Wf.d(0), FUS.d(0), FW.d(0, fmap)]
-            idx = plan.conv_fuse('merge.wp.out+fuse', self.wp_out, Bg, N, h, hw, *feats) \
+        # the base term needs only the encoder: lane 0 computes it before waiting for PWC-Net (its projections
+        # write WP channels [0, pd); the side lane writes the offset features at [pd, ..))
+        BS = self._emit_base(plan, grp, N, H, W, sh, WP) if self.wp_split is not None else None
+        plan.join(1)                      # lane 0 waits for the flow
+        plan.max_blocks = 0
+        plan.switch(1)                    # offsets are in: offset features on lane 1 ...
+        self._emit_ofe(plan, grp, N, H, W, sh, WP)
+        plan.switch(0)
+        Wf = self._emit_warp(plan, grp, N, H, W, sh, WP)      # ... beside the warp + projections
+        plan.join(1)
+        h, Wf = self._emit_merge(plan, grp, N, H, W, sh, WP, BS=BS, Wf=Wf)
+        if mode == 'partial':
+            LG = self._emit_logits(plan, B * N, H, W, h)
+            ST = torch.zeros(B, H, W, 3 * C, dtype=torch.float32, device=dev)
+            plan.add('merge.fuse_partial', lib.dbsr_fuse_partial, B, N, H * W, C, first_frame, LG.d(0),
+                     E.d(0, (1, N, 0, 1)), Wf.d(0), ST.data_ptr())
+            bufs['stats'] = ST
+        else:
+            FUS = NHWC(B, H, W, C, dt, dev)
+            feats = [E.d(0, (1, N, 0, 1)), Wf.d(0), FUS.d(0), FW.d(0)]
+            idx = plan.conv_fuse('merge.wp.out+fuse', self.wp_out, B, N, h, hw, *feats) \
                 if DBSREngine.FUSED_WP_OUT else None
             if idx is not None:
-                plan.fuse_ops.append((idx, plan.ops[idx][1], FW.d(0, fmap), None))
+                plan.fuse_ops.append((idx, plan.ops[idx][1], FW.d(0), None))
             else:
-                LG = self._emit_logits(plan, Bg * N, H, W, h)
-                args = [Bg, N, H * W, C, LG.d(0)] + feats
+                LG = self._emit_logits(plan, B * N, H, W, h)
+                args = [B, N, H * W, C, LG.d(0)] + feats
                 plan.add('merge.fuse', lib.dbsr_fuse_softmax, *args)
-                plan.fuse_ops.append((len(plan.ops) - 1, args, FW.d(0, fmap),
-                                      ((2.0 * N + 1) * Bg * C * H * W * es, 1.0 * N * Bg * C * H * W * es)))
-            self._decoder(plan, Bg, H, W, FUS, bufs, pred_out=bufs['pred'][g0:g1])
+                plan.fuse_ops.append((len(plan.ops) - 1, args, FW.d(0),
+                                      ((2.0 * N + 1) * B * C * H * W * es, 1.0 * N * B * C * H * W * es)))
+            self._decoder(plan, B, H, W, FUS, bufs, pred_out=bufs['pred'])
             plan.keep.append(FUS)
         plan.max_blocks = 0
         plan.keep.append(FW)
@@ -804,6 +771,30 @@ class DBSREngine:
             if nbytes is not None:            # (the fused conv's work stays its FLOPs)
                 plan.work[idx] = ('byte', nbytes[0] + (nbytes[1] if want else 0.0))
 
+    # Output slots per shape.  Slots 0..OUTPUT_SLOTS-2 hand out views of their static output buffers (pred,
+    # offsets, fusion weights; no copy inside the timed step) and are reused only once no tensor from their
+    # previous forward is referenced anywhere (storage use counts); the last slot is clone-only, for when
+    # the caller still holds every zero-copy slot's outputs.  Each slot is its own plan (and HIP graph).
+    OUTPUT_SLOTS = 3
+
+    @staticmethod
+    def _uses(t):
+        return torch._C._storage_Use_Count(t.untyped_storage()._cdata)
+
+    def _outputs(self, plan):
+        return [plan.bufs['pred'], plan.bufs['offsets']] + ([plan.FW.t] if plan.FW is not None else [])
+
+    def _slot_free(self, plan):
+        return all(self._uses(t) <= b for t, b in zip(self._outputs(plan), plan.out_base))
+
+    def _new_slot(self, key):
+        plan = self._build(*key)
+        plan.out_base = [self._uses(t) for t in self._outputs(plan)]
+        self.slots.setdefault(key, []).append(plan)
+        if len(self.slots[key]) == 1:
+            self.plans[key] = plan            # slot 0 is the shape's reference plan (bench.py, tests)
+        return plan
+
     def forward(self, burst):
         if not burst.is_cuda:
             raise RuntimeError('DBSRNet (MI355X engine) needs the burst on a HIP device; got %s' % burst.device)
@@ -816,39 +807,48 @@ class DBSREngine:
         if self.device != dev or self.sig != _param_signature(self.net):
             self._pack(dev)
         key = (B, N, H, W)
-        plan = self.plans.get(key)
-        if plan is None:
-            plan = self.plans[key] = self._build(B, N, H, W)
+        if key not in self.slots:
+            self._new_slot(key)
+        slots = self.slots[key]
+        nzc = DBSREngine.OUTPUT_SLOTS - 1               # zero-copy slots
+        if getattr(self.net, 'graph_zero_copy', False):
+            si = 0                                      # opt-in: always slot 0, overwritten by the next forward
+        else:
+            si = next((i for i, p in enumerate(slots[:nzc]) if self._slot_free(p)), None)
+            if si is None and len(slots) < nzc:
+                self._new_slot(key)
+                si = len(slots) - 1
+        copy = si is None
+        if copy:
+            while len(slots) < DBSREngine.OUTPUT_SLOTS:
+                self._new_slot(key)
+            si = DBSREngine.OUTPUT_SLOTS - 1
+        plan = self.slots[key][si]
         want_fw = bool(getattr(self.net, 'return_fusion_weights', True))
         self._set_fw(plan, want_fw)
         stream = L.stream_ptr(dev)
         plan.bufs['burst'].copy_(burst.to(torch.float32), non_blocking=True)
         if getattr(self.net, 'use_graph', False):
-            g = self.graphs.get((key, want_fw))
+            g = self.graphs.get((key, si, want_fw))
             if g is None:
                 plan.run(stream)                      # warm-up outside capture
                 g = self._capture(plan, dev)
-                self.graphs[(key, want_fw)] = g
+                self.graphs[(key, si, want_fw)] = g
             g.replay()
-            if getattr(self.net, 'graph_zero_copy', False):
-                # opt-in: views of the plan's static buffers, overwritten by the next forward of this shape
-                pred, offs = plan.bufs['pred'], plan.bufs['offsets']
-                fw_t = plan.FW.t if want_fw else None
-            else:
-                pred, offs = plan.bufs['pred'].clone(), plan.bufs['offsets'].clone()
-                fw_t = plan.FW.t.clone() if want_fw else None
         else:
             plan.run(stream)
-            pred, offs = plan.bufs['pred'].clone(), plan.bufs['offsets'].clone()
-            fw_t = plan.FW.t.clone() if want_fw else None
+        pred, offs = plan.bufs['pred'], plan.bufs['offsets']
+        fw_t = plan.FW.t if want_fw else None
+        if copy:
+            pred, offs = pred.clone(), offs.clone()
+            fw_t = fw_t.clone() if want_fw else None
         aux = {'offsets': offs.view(B, N - 1, 2, H, W)}
         if want_fw:
             # [B*N,H,W,C] channels-last storage viewed as the reference's [B,N,C,H,W]
             aux['fusion_weights'] = fw_t.view(B, N, H, W, -1).permute(0, 1, 4, 2, 3)
         else:
             aux['fusion_weights'] = None
-        return pred, aux
-
+        return pred.view(pred.shape), aux
 
     # ---------------- frame-sharded fusion (BASELINE configs[4]) ----------------
     def _build_combine(self, R, B, H, W):

@@ -66,6 +66,9 @@ def _register_autograd():
 
     def fuse_setup(ctx, inputs, output):
         logits, feats, want = inputs
+        if feats.shape[2] % 8:
+            # the forward kernel takes C % 4, the backward C % 8: fail while recording, not in backward()
+            raise RuntimeError('dbsr::fuse_softmax: autograd needs C % 8 == 0 (got C = %d)' % feats.shape[2])
         fused, weights = output
         if weights.numel() == 0:           # weights are needed for the backward: recompute them
             _, weights = torch.ops.dbsr.fuse_softmax(logits, feats, True)

@@ -102,6 +102,10 @@ class DBSRTrainer:
         if dev.type != 'cuda':
             raise RuntimeError('DBSRTrainer needs the network on a HIP device')
         self.net, self.dev, self.dtype = net, dev, net.compute_dtype
+        if self.dtype == torch.float16:
+            # no loss scaling: the L1 gradient 1/count (~4.7e-8 at configs[3]) is below fp16's smallest
+            # subnormal, so an fp16 backward would underflow to zero
+            raise ValueError('DBSRTrainer: train in torch.bfloat16 or torch.float32 (fp16 has no loss scaling here)')
         self.lr, self.betas, self.eps, self.bi = lr, betas, eps, boundary_ignore
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if (dist.is_available() and dist.is_initialized()) else 1
@@ -455,7 +459,7 @@ class DBSRTrainer:
                                        self.betas[1], self.eps, self.step_count, 1.0 / self.world, stream), 'adam')
         # the inference engine packs from the module parameters (now updated in place): repack next forward
         self.net._engine = None
-        return self.loss
+        return self.loss.clone()          # (self.loss is the plan's buffer, overwritten by the next step)
 
     def forward_backward(self, burst, frame_gt):
         """Loss and gradients only (no all-reduce, no optimizer step): for tests."""

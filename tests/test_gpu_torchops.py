@@ -101,3 +101,38 @@ def test_conv2d_fused_op(dbsr, dtype):
     out2 = dbsr.conv2d_fused(x.to(DEV).to(dtype), wd, b.to(DEV), 1, 1, 1, 1, r.to(DEV).to(dtype), 1).float().cpu()
     ref2 = F.relu(F.relu(F.conv2d(xr, (w * 0.5).to(dtype).float(), b, padding=1)) + rr)
     assert _rel(out2, ref2) <= tol
+
+
+def test_conv2d_fused_cache_bias_and_address_reuse(dbsr):
+    """the packed-weight cache must not serve (a) a bias-less packing to a call with a bias,
+    (b) one weight's packing to another weight that reuses its address, (c) stale entries of freed weights."""
+    gen = torch.Generator().manual_seed(21)
+    x = torch.randn(1, 32, 8, 8, generator=gen)
+    b = torch.randn(16, generator=gen)
+    xd = x.to(DEV)
+    torch.ops.dbsr.clear_pack_cache()
+    w = torch.randn(16, 32, 3, 3, generator=gen) / 17.0
+    wd = w.to(DEV)
+    o0 = dbsr.conv2d_fused(xd, wd, None, 1, 1, 1, 0, None, 0).cpu()
+    o1 = dbsr.conv2d_fused(xd, wd, b.to(DEV), 1, 1, 1, 0, None, 0).cpu()
+    assert _rel(o0, F.conv2d(x, w, None, padding=1)) <= 1e-4
+    assert _rel(o1, F.conv2d(x, w, b, padding=1)) <= 1e-4
+    b2 = b.to(DEV)
+    o2 = dbsr.conv2d_fused(xd, wd, b2, 1, 1, 1, 0, None, 0).cpu()
+    with torch.no_grad():
+        b2.add_(1.0)                                     # bias update -> repack
+    o3 = dbsr.conv2d_fused(xd, wd, b2, 1, 1, 1, 0, None, 0).cpu()
+    assert _rel(o2, F.conv2d(x, w, b, padding=1)) <= 1e-4
+    assert _rel(o3, F.conv2d(x, w, b + 1.0, padding=1)) <= 1e-4
+    # fresh weights allocated in a loop reuse the caching allocator's address, all at version 0
+    ptrs = set()
+    for i in range(4):
+        cout = 16 if i % 2 == 0 else 24
+        wi = torch.randn(cout, 32, 3, 3, generator=gen) / 17.0
+        wdi = wi.to(DEV)
+        ptrs.add(wdi.data_ptr())
+        oi = dbsr.conv2d_fused(xd, wdi, None, 1, 1, 1, 0, None, 0).cpu()
+        assert oi.shape[1] == cout
+        assert _rel(oi, F.conv2d(x, wi, None, padding=1)) <= 1e-4, i
+        del wdi
+    assert torch.ops.dbsr.pack_cache_size() <= 2         # freed weights' entries are evicted

@@ -181,3 +181,36 @@ def test_gloo_world2_ddp_gradients_equal_single_process():
     for rank, err, covers in res:
         assert covers                      # the three buckets cover every trainable parameter
         assert err <= 1e-5, (rank, err)
+
+
+def test_bench_launcher_spawns_ranks_gloo():
+    """bench.py --gpus N outside torchrun starts N rank processes itself (before any GPU call) and every rank
+    derives the same tiling of the global batch (admin/multigpu.py:8-14 is the reference's
+    single-process DataParallel).  --dry-run swaps the GPU work for a gloo all-gather of the shards."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK')}
+    for n in (2, 3):
+        out = subprocess.run([sys.executable, os.path.join(repo, 'bench.py'), '--gpus', str(n), '--batch', '8',
+                              '--dry-run'], capture_output=True, text=True, timeout=240, env=env, cwd=repo)
+        assert out.returncode == 0, out.stderr[-2000:]
+        line = [ln for ln in out.stdout.splitlines() if ln.startswith('{')][-1]
+        res = json.loads(line)
+        assert res['n_gpus'] == n and res['global_batch'] == 8 * n
+        ranks = sorted(res['ranks'])
+        assert [r[0] for r in ranks] == list(range(n)) and all(r[1] == n for r in ranks)
+        assert ranks[0][2] == 0 and ranks[-1][3] == 8 * n
+        assert all(a[3] == b[2] for a, b in zip(ranks, ranks[1:]))       # contiguous, no overlap
+        assert all(r[3] - r[2] == 8 for r in ranks)                      # weak scaling: --batch per rank
+
+
+def test_bench_rejects_gpus_world_mismatch():
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE='1', RANK='0', LOCAL_RANK='0')
+    out = subprocess.run([sys.executable, os.path.join(repo, 'bench.py'), '--gpus', '2', '--dry-run'],
+                         capture_output=True, text=True, timeout=120, env=env, cwd=repo)
+    assert out.returncode != 0 and 'one rank per GPU' in out.stderr

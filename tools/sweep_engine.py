@@ -1,5 +1,5 @@
 """A/B the engine's scheduling knobs on the bench workload.
-Usage: python tools/sweep_engine.py 'LANE0_CU_SHARE=0.5,PIPELINE_GROUPS=1' 'PIPELINE_GROUPS=2' 'Plan.MULTI_STREAM=0' ...
+Usage: python tools/sweep_engine.py 'LANE0_CU_SHARE=0.5' 'LANE0_CU_SHARE=0.625' 'Plan.MULTI_STREAM=0' ...
 Each argument is one configuration of DBSREngine (or Plan.*) class attributes; prints bursts/s per configuration."""
 import json
 import os
