@@ -36,7 +36,7 @@ PEAK_MFMA_TFLOPS = {'bf16': 2500.0, 'fp16': 2500.0, 'fp32': 157.3}   # dense pea
 DTYPES = {'bf16': 'bfloat16', 'fp16': 'float16', 'fp32': 'float32'}
 # conv-like kernel families (MFMA-bound; bench reports each against the dense peak)
 CONV_FAMILIES = ('conv3x3_ws', 'conv3x3_pipe', 'conv3x3_tiled', 'conv2d_generic', 'conv1x1', 'conv1x1_shuffle',
-                 'conv_fuse', 'pwc_dense')
+                 'conv_fuse', 'pwc_dense', 'pwc_extract')
 KERNEL_DESC = {'conv3x3_ws': 'conv3x3_ws_kernel (persistent weight-stationary implicit-GEMM 3x3, Cin <= 64',
                'conv3x3_pipe': 'conv3x3_pipe_kernel (persistent LDS-DMA-pipelined implicit-GEMM 3x3',
                'conv3x3_tiled': 'conv3x3_tiled_kernel (LDS-tiled implicit-GEMM 3x3',
@@ -44,7 +44,8 @@ KERNEL_DESC = {'conv3x3_ws': 'conv3x3_ws_kernel (persistent weight-stationary im
                'conv1x1': 'conv1x1_kernel (pointwise projection, LDS-resident weights',
                'conv1x1_shuffle': 'upsample_shuffle_kernel (1x1 conv + PixelShuffle',
                'conv_fuse': 'conv_fuse_kernel (weight-predictor output conv + softmax + fusion',
-               'pwc_dense': 'pwc_dense_kernel (PWC-Net DenseNet decoder level in one launch'}
+               'pwc_dense': 'pwc_dense_kernel (PWC-Net DenseNet decoder level in one launch',
+               'pwc_extract': 'pwc_extract_kernel (PWC-Net feature pyramid in one launch'}
 # PMC traffic per launch of each kernel family, from the committed rocprofv3 --pmc passes of this same
 # command (tools/profile.sh -> tools/summarize_profile.py); bench.py cannot read its own counters
 TRAFFIC_FILE = os.path.join(REPO, 'profiles', 'pmc_traffic.json')

@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get('DBSR_HIP_LIB', os.path.join(_HERE, 'libdbsr_hip.so'))
 DBSR_F32, DBSR_BF16, DBSR_F16 = 0, 1, 2
 ACT_NONE, ACT_RELU, ACT_LRELU = 0, 1, 2
 OUT_NHWC, OUT_SHUFFLE, OUT_NCHW_F32 = 0, 1, 2
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 
 class FrameMap(ctypes.Structure):
@@ -35,6 +35,12 @@ class PwcDenseConv(ctypes.Structure):
     """dbsr_pwc_dense_conv (include/dbsr_hip.h)."""
     _fields_ = [('w', ctypes.c_void_p), ('bias', ctypes.c_void_p), ('kp', ctypes.c_int), ('cg', ctypes.c_int),
                 ('start', ctypes.c_int), ('cout', ctypes.c_int), ('out_off', ctypes.c_int)]
+
+
+class PwcExtConv(ctypes.Structure):
+    """dbsr_pwc_ext_conv (include/dbsr_hip.h)."""
+    _fields_ = [('w', ctypes.c_void_p), ('bias', ctypes.c_void_p), ('cin', ctypes.c_int), ('cout', ctypes.c_int),
+                ('stride', ctypes.c_int)]
 
 
 class ConvDesc(ctypes.Structure):
@@ -118,6 +124,11 @@ def lib():
             'dbsr_dgrad_weights': ([c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p], c_int),
             'dbsr_pwc_dense': ([c_int, c_int, c_int, Tensor, c_int, c_void_p, Tensor, c_void_p], c_int),
             'dbsr_pwc_dense_supported': ([c_int, c_int, c_int], c_int),
+            'dbsr_pwc_extract': ([c_int, c_int, c_int, Tensor, c_void_p, c_void_p, c_void_p], c_int),
+            'dbsr_pwc_extract_supported': ([c_int, c_int], c_int),
+            'dbsr_pwc_level_prep': ([c_int, c_int, c_int, c_int, c_float, Tensor, Tensor, Tensor, Tensor, c_int, Tensor,
+                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
+            'dbsr_pwc_level_prep_supported': ([c_int, c_int, c_int], c_int),
             'dbsr_resize_bilinear': ([c_int, c_int, c_int, c_void_p, c_int, c_int, c_float, c_float, c_float, c_void_p,
                                       c_void_p], c_int),
             'dbsr_gauss_reflect': ([c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
@@ -146,7 +157,8 @@ EXPORTED = ['dbsr_abi_version', 'dbsr_last_error', 'dbsr_conv_packed_elems', 'db
             'dbsr_fuse_backward', 'dbsr_merge_prep_backward', 'dbsr_warp_backward', 'dbsr_enc_grad_gate',
             'dbsr_adam_step', 'dbsr_dgrad_weights',
             'dbsr_resize_bilinear', 'dbsr_gauss_reflect', 'dbsr_color_fit', 'dbsr_color_apply', 'dbsr_pwc_dense',
-            'dbsr_pwc_dense_supported']
+            'dbsr_pwc_dense_supported', 'dbsr_pwc_extract', 'dbsr_pwc_extract_supported',
+            'dbsr_pwc_level_prep', 'dbsr_pwc_level_prep_supported']
 
 
 def check(rc, what):

@@ -299,6 +299,8 @@ def _param_signature(module):
 class PWCPlanner:
     """Packs PWC-Net weights and emits the PWC part of a plan (pwcnet.py:221-231 + :262-279)."""
     FUSED_DENSE = True        # 16-bit coarse levels (<= 64 pixels per pair): dbsr_pwc_dense
+    FUSED_EXTRACT = True      # 16-bit 64x64 frames: the whole feature pyramid in one launch (dbsr_pwc_extract)
+    FUSED_PREP = True         # 16-bit: each decoder level's ConvTs, backwarp, correlation, assembly in one launch
     def __init__(self, pwc_module, W):
         net = pwc_module.net
         ex = net.netExtractor
@@ -314,6 +316,12 @@ class PWCPlanner:
             if level < 6:
                 ent['upflow'] = pack_convt(d.netUpflow, W.device)
                 ent['upfeat'] = pack_convt(d.netUpfeat, W.device)
+                if W.dtype != torch.float32:
+                    # 16-bit rows [(ky*4+kx)*2 + co][cin32] for dbsr_pwc_level_prep's MFMA ConvT
+                    wt = ent['upfeat'][0]
+                    cin = wt.shape[-1]
+                    ent['upfeat16'] = torch.nn.functional.pad(wt.reshape(32, cin), (0, (cin + 31) // 32 * 32 - cin)) \
+                        .to(W.dtype).contiguous()
             self.dec[level] = ent
         self.ref = [W.conv(net.netRefiner.netMain[i]) for i in range(0, 13, 2)]
 
@@ -324,20 +332,39 @@ class PWCPlanner:
         lib = L.lib()
         # ---- feature pyramid (Extractor.forward, pwcnet.py:103-111), once per frame ----
         levels = {}
-        x, hw = rgb, (Hp, Wp)
-        for k in range(6):
-            C = PWC_LEVEL_CH[k + 1]
-            oh, ow = self.ext[k][0].out_hw(*hw)
-            ta = NHWC(nF, oh, ow, cpad(C), dtype, device)
-            tb = NHWC(nF, oh, ow, cpad(C), dtype, device)
-            lv = NHWC(nF, oh, ow, cpad(C), dtype, device)
-            plan.conv(f'pwc.ext{k + 1}.0', self.ext[k][0], nF, x, 0, hw, ta, 0, L.ACT_LRELU,
-                      xmap=rgb_map if k == 0 else IDENTITY)
-            plan.conv(f'pwc.ext{k + 1}.2', self.ext[k][1], nF, ta, 0, (oh, ow), tb, 0, L.ACT_LRELU)
-            plan.conv(f'pwc.ext{k + 1}.4', self.ext[k][2], nF, tb, 0, (oh, ow), lv, 0, L.ACT_LRELU)
-            levels[k + 1] = lv
-            plan.keep.extend([ta, tb])      # every buffer a launch touches lives as long as the plan
-            x, hw = lv, (oh, ow)
+        if PWCPlanner.FUSED_EXTRACT and dtype != torch.float32 and lib.dbsr_pwc_extract_supported(Hp, Wp):
+            # all six levels in one launch, activations in LDS (csrc/pwc_fused.hip)
+            convs = (L.PwcExtConv * 18)()
+            lv = (L.Tensor * 6)()
+            hw, flop = (Hp, Wp), 0.0
+            for k in range(6):
+                C = PWC_LEVEL_CH[k + 1]
+                oh, ow = self.ext[k][0].out_hw(*hw)
+                levels[k + 1] = NHWC(nF, oh, ow, cpad(C), dtype, device)
+                lv[k] = levels[k + 1].d(0)
+                for j in range(3):
+                    pc = self.ext[k][j]
+                    convs[3 * k + j] = L.PwcExtConv(pc.w.data_ptr(), pc.bias.data_ptr(), pc.cin, pc.cout, pc.stride)
+                    flop += 2.0 * nF * oh * ow * pc.cout * pc.cin * 9
+                hw = (oh, ow)
+            plan.keep.extend([convs, lv])
+            plan.add('pwc.extract', lib.dbsr_pwc_extract, nF, Hp, Wp, rgb.d(0, rgb_map), convs, lv, work=('flop', flop))
+            plan.kernel[len(plan.ops) - 1] = 'pwc_extract'
+        else:
+            x, hw = rgb, (Hp, Wp)
+            for k in range(6):
+                C = PWC_LEVEL_CH[k + 1]
+                oh, ow = self.ext[k][0].out_hw(*hw)
+                ta = NHWC(nF, oh, ow, cpad(C), dtype, device)
+                tb = NHWC(nF, oh, ow, cpad(C), dtype, device)
+                lv = NHWC(nF, oh, ow, cpad(C), dtype, device)
+                plan.conv(f'pwc.ext{k + 1}.0', self.ext[k][0], nF, x, 0, hw, ta, 0, L.ACT_LRELU,
+                          xmap=rgb_map if k == 0 else IDENTITY)
+                plan.conv(f'pwc.ext{k + 1}.2', self.ext[k][1], nF, ta, 0, (oh, ow), tb, 0, L.ACT_LRELU)
+                plan.conv(f'pwc.ext{k + 1}.4', self.ext[k][2], nF, tb, 0, (oh, ow), lv, 0, L.ACT_LRELU)
+                levels[k + 1] = lv
+                plan.keep.extend([ta, tb])      # every buffer a launch touches lives as long as the plan
+                x, hw = lv, (oh, ow)
         plan.keep.append(levels)
         # ---- decoders, coarse to fine (pwcnet.py:225-229, Decoder.forward :153-184) ----
         prev = None
@@ -348,27 +375,40 @@ class PWCPlanner:
             ld = BASE_OFF + cpad(base_real)
             D = NHWC(P, h, w, ld, dtype, device)
             ent = self.dec[level]
-            if prev is None:
-                second = feat.d(0, second_map)
+            if PWCPlanner.FUSED_PREP and dtype != torch.float32 and lib.dbsr_pwc_level_prep_supported(h, w, C):
+                # ConvT x2 + backwarp + correlation + assembly in one launch (csrc/pwc_fused.hip)
+                if prev is None:
+                    pargs = (L.NULL_TENSOR, 0, L.NULL_TENSOR, None, None, None, None)
+                else:
+                    pD, pflow, pbase = prev
+                    wf, bf = ent['upflow']
+                    bt = ent['upfeat'][1]
+                    pargs = (pD.d(0), BASE_OFF + pbase, pflow.d(0), wf.data_ptr(), bf.data_ptr(),
+                             ent['upfeat16'].data_ptr(), bt.data_ptr())
+                plan.add(f'pwc.dec{level}.prep', lib.dbsr_pwc_level_prep, P, h, w, C, BACKWARP_SCALE.get(level, 1.0),
+                         feat.d(0, first_map), feat.d(0, second_map), D.d(BASE_OFF), *pargs)
             else:
-                pD, pflow, pbase = prev
-                fu = NHWC(P, h, w, 8, torch.float32, device)     # upflow (2 ch; ld 8 for the 8-wide ConvT reads)
-                fe = NHWC(P, h, w, 2, torch.float32, device)     # upfeat
-                wt, bs = ent['upflow']
-                plan.add(f'pwc.dec{level}.upflow', lib.dbsr_conv_transpose_k4s2, P, pD.h, pD.w, 2, 2, pflow.d(0),
-                         wt.data_ptr(), bs.data_ptr(), fu.d(0))
-                wt, bs = ent['upfeat']
-                plan.add(f'pwc.dec{level}.upfeat', lib.dbsr_conv_transpose_k4s2, P, pD.h, pD.w, BASE_OFF + pbase, 2,
-                         pD.d(0), wt.data_ptr(), bs.data_ptr(), fe.d(0))
-                ws = NHWC(P, h, w, cpad(C), dtype, device)
-                plan.add(f'pwc.dec{level}.backwarp', lib.dbsr_backwarp, P, h, w, C, feat.d(0, second_map), fu.d(0),
-                         BACKWARP_SCALE[level], ws.d(0))
-                plan.add(f'pwc.dec{level}.assemble', lib.dbsr_pwc_assemble, P, h, w, C, feat.d(0, first_map), fu.d(0),
-                         fe.d(0), D.d(BASE_OFF))
-                second = ws.d(0)
-                plan.keep.extend([fu, fe, ws])
-            plan.add(f'pwc.dec{level}.corr', lib.dbsr_correlation, P, h, w, C, feat.d(0, first_map), second,
-                     D.d(BASE_OFF), 1)
+                if prev is None:
+                    second = feat.d(0, second_map)
+                else:
+                    pD, pflow, pbase = prev
+                    fu = NHWC(P, h, w, 8, torch.float32, device)     # upflow (2 ch; ld 8 for the 8-wide ConvT reads)
+                    fe = NHWC(P, h, w, 2, torch.float32, device)     # upfeat
+                    wt, bs = ent['upflow']
+                    plan.add(f'pwc.dec{level}.upflow', lib.dbsr_conv_transpose_k4s2, P, pD.h, pD.w, 2, 2, pflow.d(0),
+                             wt.data_ptr(), bs.data_ptr(), fu.d(0))
+                    wt, bs = ent['upfeat']
+                    plan.add(f'pwc.dec{level}.upfeat', lib.dbsr_conv_transpose_k4s2, P, pD.h, pD.w, BASE_OFF + pbase,
+                             2, pD.d(0), wt.data_ptr(), bs.data_ptr(), fe.d(0))
+                    ws = NHWC(P, h, w, cpad(C), dtype, device)
+                    plan.add(f'pwc.dec{level}.backwarp', lib.dbsr_backwarp, P, h, w, C, feat.d(0, second_map), fu.d(0),
+                             BACKWARP_SCALE[level], ws.d(0))
+                    plan.add(f'pwc.dec{level}.assemble', lib.dbsr_pwc_assemble, P, h, w, C, feat.d(0, first_map),
+                             fu.d(0), fe.d(0), D.d(BASE_OFF))
+                    second = ws.d(0)
+                    plan.keep.extend([fu, fe, ws])
+                plan.add(f'pwc.dec{level}.corr', lib.dbsr_correlation, P, h, w, C, feat.d(0, first_map), second,
+                         D.d(BASE_OFF), 1)
             fl = NHWC(P, h, w, 8, torch.float32, device)    # 2 ch (ld 8: read by the next level's ConvT)
             if PWCPlanner.FUSED_DENSE and dtype != torch.float32 and lib.dbsr_pwc_dense_supported(h, w, ld):
                 # coarse level: the DenseNet + flow conv in one launch with D in LDS (csrc/pwc_dense.hip)

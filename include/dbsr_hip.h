@@ -27,6 +27,8 @@
  *   dbsr_gauss_blur3          upsampling.py:59-65 (depthwise Gaussian, zero padding)
  *   dbsr_merge_prep           merging.py:79-89 (base_feat_proj, feat_diff_proj)
  *   dbsr_pwc_assemble         pwcnet.py:171 (cat([tenVolume, tenFirst, tenFlow, tenFeat]))
+ *   dbsr_pwc_extract          pwcnet.py:45-111 (Extractor: the whole six-level feature pyramid)
+ *   dbsr_pwc_level_prep       pwcnet.py:153-171 (a decoder level's ConvTs, backwarp, correlation, cat)
  */
 #ifndef DBSR_HIP_H
 #define DBSR_HIP_H
@@ -38,7 +40,7 @@
 extern "C" {
 #endif
 
-#define DBSR_ABI_VERSION 10
+#define DBSR_ABI_VERSION 11
 
 enum { DBSR_F32 = 0, DBSR_BF16 = 1, DBSR_F16 = 2 };
 enum { DBSR_ACT_NONE = 0, DBSR_ACT_RELU = 1, DBSR_ACT_LRELU = 2 };      /* LeakyReLU slope 0.1 */
@@ -222,6 +224,33 @@ int dbsr_pwc_dense(int P, int h, int w, dbsr_tensor D, int dense_ch, const dbsr_
                    dbsr_tensor flow, void* stream);
 /* 1 if dbsr_pwc_dense has an LDS tile for an h x w level with ld channels in D (else use dbsr_conv2d). */
 int dbsr_pwc_dense_supported(int h, int w, int ld);
+
+/* The PWC-Net feature pyramid (Extractor.forward, pwcnet.py:103-111) of F 64x64 frames in one launch:
+ * convs[3l + j] = level l+1's conv j (j = 0: 3x3 stride 2, j = 1, 2: 3x3 stride 1), channels 3 -> 16 -> 32 ->
+ * 64 -> 96 -> 128 -> 196, each + bias + LeakyReLU(0.1); weights packed by dbsr_conv_pack_weights (16-bit).
+ * rgb: the 8-channel packed frames [F][64][64] (dbsr_pack_burst); levels[l]: NHWC [F][64 >> (l+1)]^2 with
+ * ld = the padded width (16, 32, 64, 96, 128, 224), written in full (pad channels as zeros).
+ * Requires dbsr_pwc_extract_supported(Hp, Wp) (Hp = Wp = 64) and 16-bit activations. */
+typedef struct {
+    const void* w;
+    const float* bias;
+    int cin, cout, stride;
+} dbsr_pwc_ext_conv;
+int dbsr_pwc_extract(int F, int Hp, int Wp, dbsr_tensor rgb, const dbsr_pwc_ext_conv* convs,
+                     const dbsr_tensor* levels, void* stream);
+int dbsr_pwc_extract_supported(int Hp, int Wp);
+/* One PWC decoder level's input (Decoder.forward, pwcnet.py:153-171) in one launch, per pair p:
+ * upflow = ConvT(prev_flow), upfeat = ConvT(prev_D channels [0, prev_cin)) (k4 s2 p1; w_upflow as for
+ * dbsr_conv_transpose_k4s2, fp32 [4][4][2][8]; w_upfeat 16-bit (D's dtype) [4][4][2][round_up(prev_cin, 32)],
+ * i.e. rows (ky*4+kx)*2+co, zero-padded channels), warped = backwarp(second, upflow * scale) (dbsr_backwarp),
+ * D[c0 + 0..80] = LeakyReLU(correlation(first, warped)) (dbsr_correlation), D[c0 + 81 ..] = [first | upflow |
+ * upfeat] (dbsr_pwc_assemble).  prev_D.ptr == NULL: the coarsest level (no warp, correlation only).  first /
+ * second: 16-bit level features (c0 0, ld >= the padded width) with pair -> frame maps; D: 16-bit, c0 = the
+ * base channels.  Requires dbsr_pwc_level_prep_supported(h, w, c) (the level fits one block's LDS). */
+int dbsr_pwc_level_prep(int P, int h, int w, int c, float scale, dbsr_tensor first, dbsr_tensor second, dbsr_tensor D,
+                        dbsr_tensor prev_D, int prev_cin, dbsr_tensor prev_flow, const float* w_upflow,
+                        const float* b_upflow, const void* w_upfeat, const float* b_upfeat, void* stream);
+int dbsr_pwc_level_prep_supported(int h, int w, int c);
 
 /* ---------------- BurstSR scoring: SpatialColorAlignment (spatial_color_alignment.py:23-108) ----------------
  * fp32 NCHW planes.  rh / rw are PyTorch's internal source-coordinate ratios, 1 / scale_factor. */

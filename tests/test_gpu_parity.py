@@ -359,3 +359,39 @@ def test_pwc_fused_dense_levels(synth_sd, dtype):
     print('fused err %.4g unfused err %.4g diff %.4g (|flow| max %.3g)' % (e_f, e_u, d, scale))
     assert e_f <= max(1.5 * e_u, 2e-3 * scale)
     assert d <= 0.02 * scale
+
+
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
+def test_pwc_fused_extractor(synth_sd, dtype):
+    """The one-launch feature pyramid (dbsr_pwc_extract, pwcnet.py:45-111) against the per-conv path on the same
+    16-bit inputs and both against the fp32 oracle PWC-Net: 48x56 frames (resized to 64x64, pwcnet.py:262-271),
+    the flows may differ only by summation order / 16-bit rounding placement."""
+    from dbsr_amd.engine import PWCPlanner
+    from dbsr_amd.pwcnet import PWCNet
+    from oracle import dbsr_oracle as orc
+    pre = 'encoder.alignment_net.'
+    gen = torch.Generator().manual_seed(15)
+    src = torch.rand(10, 3, 48, 56, generator=gen)
+    tgt = (src + 0.05 * torch.randn(10, 3, 48, 56, generator=gen)).clamp(0, 1)
+    ref = orc.pwcnet(src, tgt, synth_sd)
+    flows = {}
+    try:
+        for fused in (True, False):
+            PWCPlanner.FUSED_EXTRACT = fused
+            net = PWCNet(load_pretrained=False)
+            net.load_state_dict({k[len(pre):]: v for k, v in synth_sd.items() if k.startswith(pre)})
+            net = net.to(DEV)
+            net.compute_dtype = dtype
+            with torch.no_grad():
+                flows[fused] = net(src.to(DEV), tgt.to(DEV)).cpu()
+            names = [n for _, _, n, _ in next(iter(net._engine.plans.values())).ops]
+            assert ('pwc.extract' in names) == fused, names
+    finally:
+        PWCPlanner.FUSED_EXTRACT = True
+    e_f = (flows[True] - ref).abs().max().item()
+    e_u = (flows[False] - ref).abs().max().item()
+    d = (flows[True] - flows[False]).abs().max().item()
+    scale = ref.abs().max().item()
+    print('fused extractor err %.4g unfused err %.4g diff %.4g (|flow| max %.3g)' % (e_f, e_u, d, scale))
+    assert e_f <= max(1.5 * e_u, 2e-3 * scale)
+    assert d <= 0.02 * scale
