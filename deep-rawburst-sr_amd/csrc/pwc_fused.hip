@@ -18,6 +18,7 @@
 
 #include <algorithm>
 #include <type_traits>
+#include <utility>
 
 using namespace dbsr;
 
@@ -36,184 +37,302 @@ __device__ __forceinline__ f32x4_t mfma16(bf16x8_t a, bf16x8_t b, f32x4_t c) {
                                                       0, 0, 0);
 }
 
-inline int round_up_i(int a, int b) { return (a + b - 1) / b * b; }
-inline int cpad_i(int c) { return c <= 16 ? round_up_i(c, 8) : round_up_i(c, 32); }
-// LDS pixel stride of an image with c channels: the padded width (+8 above 16 channels, which spreads the
-// 16 pixel rows of a B-fragment read over the banks)
-inline int lds_ld(int c) { return cpad_i(c) <= 16 ? cpad_i(c) : cpad_i(c) + 8; }
+inline int cpad_i(int c) { return c <= 16 ? (c + 7) / 8 * 8 : (c + 31) / 32 * 32; }
 
 constexpr int EXT_CONVS = 18;
 constexpr int EXT_R0 = 66 * 66 * 8;                 // input frame, bordered, 8 channels
 constexpr int EXT_R1 = 34 * 34 * 16;                // level-1 images, bordered, 16 channels
 constexpr int EXT_ELEMS = EXT_R0 + 2 * EXT_R1;      // 143.7 KiB of 16-bit elements
 
-struct ExtConv {
-    const void* w;
-    const float* bias;
-    int Kp, CG, KG;          // packed row length, 8-channel groups per tap, real k-groups (9 * CG)
-    int ks_lo, ks_hi;        // k-steps that contain an in-frame tap
-    int mt, cout;            // 16-cout M tiles (padded width / 16), real couts
-    int stride;
-    int ih, iw, ild;         // input image (interior size) and its LDS pixel stride
-    int oh, ow, old;         // output image
-    int in_buf, out_buf;     // LDS images 0 (input frame), 1, 2
-    int level;               // >= 0: also store to the level output tensor
+__host__ __device__ constexpr int ext_ch(int l) {   // channels of pyramid level l (0 = the RGB input), pwcnet.py:49-100
+    return l == 0 ? 3 : l == 1 ? 16 : l == 2 ? 32 : l == 3 ? 64 : l == 4 ? 96 : l == 5 ? 128 : 196;
+}
+__host__ __device__ constexpr int cpad_c(int c) { return c <= 16 ? (c + 7) / 8 * 8 : (c + 31) / 32 * 32; }
+__host__ __device__ constexpr int ldsld_c(int c) { return cpad_c(c) <= 16 ? cpad_c(c) : cpad_c(c) + 8; }
+// does tap offset k (0..2) of a stride-s, pad-1 conv see an in-frame input pixel for some output pixel?
+__host__ __device__ constexpr bool tap_live(int k, int s, int ih, int oh) {
+    bool ok = false;
+    for (int o = 0; o < oh; ++o) ok = ok || (o * s - 1 + k >= 0 && o * s - 1 + k < ih);
+    return ok;
+}
+__host__ __device__ constexpr int tap_lo(int s, int ih, int oh) {
+    int lo = 9;
+    for (int t = 8; t >= 0; --t)
+        if (tap_live(t / 3, s, ih, oh) && tap_live(t % 3, s, ih, oh)) lo = t;
+    return lo;
+}
+__host__ __device__ constexpr int tap_hi(int s, int ih, int oh) {
+    int hi = -1;
+    for (int t = 0; t < 9; ++t)
+        if (tap_live(t / 3, s, ih, oh) && tap_live(t % 3, s, ih, oh)) hi = t;
+    return hi;
+}
+
+// Compile-time geometry of conv I of the pyramid (level I / 3, conv I % 3)
+template <int I> struct ExtSpec {
+    static constexpr int L = I / 3, J = I % 3;
+    static constexpr int CIN = J == 0 ? ext_ch(L) : ext_ch(L + 1), COUT = ext_ch(L + 1), S = J == 0 ? 2 : 1;
+    static constexpr int IH = J == 0 ? (64 >> L) : (64 >> (L + 1)), OH = 64 >> (L + 1);
+    static constexpr int IBW = IH + 2, OBW = OH + 2;
+    static constexpr int ILD = I == 0 ? 8 : ldsld_c(CIN), OLD = ldsld_c(COUT);
+    static constexpr int IN_BUF = I == 0 ? 0 : ((I - 1) % 2 == 0 ? 1 : 2), OUT_BUF = I % 2 == 0 ? 1 : 2;
+    static constexpr int CG = cpad_c(CIN) / 8;
+    static constexpr int KP = (9 * CG + 3) / 4 * 4 * 8;                  // packed row length
+    static constexpr bool PIPE = CIN > 16;                                // chunk-major copy (1-KiB pieces)
+    static constexpr int NCH = cpad_c(CIN) / 32;
+    static constexpr int TLO = tap_lo(S, IH, OH), THI = tap_hi(S, IH, OH), NTAP = THI - TLO + 1;
+    static constexpr int KS_LO = PIPE ? 0 : (TLO * CG) / 4;
+    static constexpr int NKS = PIPE ? NCH * NTAP : ((THI + 1) * CG + 3) / 4 - KS_LO;
+    static constexpr int MT = cpad_c(COUT) / 16, NPIX = OH * OH, NT = (NPIX + 15) / 16;
+    static constexpr int P = COUT <= 32 ? 32 : 64;                        // pipe_cout_perm tile
+    static constexpr bool FIXED_M = 8 % MT == 0;
+    static constexpr int WPIPE = (COUT + 63) / 64 * 64 * KP;              // offset of the chunk-major copy
+    static_assert(NTAP >= 1 && NKS >= 1, "no live tap");
+    static_assert((OH + 2) * (OH + 2) * OLD <= EXT_R1, "output image exceeds its LDS buffer");
 };
 
 struct ExtArgs {
     int F;
-    dbsr_tensor rgb;         // [F][64][64][8]
-    dbsr_tensor lv[6];       // level outputs [F][64 >> (l+1)]^2 [cpad(C_l)]
-    ExtConv cv[EXT_CONVS];
+    dbsr_tensor rgb;                   // [F][64][64][8]
+    dbsr_tensor lv[6];                 // level outputs [F][64 >> (l+1)]^2 [cpad(C_l)]
+    const void* w[EXT_CONVS];          // packed weights (row layout, then the chunk-major copy for cin > 16)
+    const float* bias[EXT_CONVS];
 };
+
+// Diagnostic build only (make exp EXP_FLAGS=-DDBSR_EXT_STAMPS): s_memtime per wave after every conv's barrier
+// and after its compute, read back by dbsr_diag_ext_stamps (tools/ext_stamps.py).
+#ifdef DBSR_EXT_STAMPS
+__device__ unsigned long long g_ext_stamps[128 * 8 * 40];
+#define EXT_STAMP(slot) do { if (c.lane == 0 && blockIdx.x < 128) g_ext_stamps[(blockIdx.x * 8 + c.wave) * 40 + (slot)] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define EXT_STAMP(slot) do { } while (0)
+#endif
+
+template <typename T> struct ExtCtx {
+    const ExtArgs* a;
+    T* base;
+    int f, lane, wave, kgl, col;
+    bf16x8_t pa[2][16];                // A-fragment sets: conv I computes from set I % 2, prefetches set (I+1) % 2
+    float pb[2][4];
+    __device__ T* img(int b) const { return base + (b == 0 ? 0 : b == 1 ? EXT_R0 : EXT_R0 + EXT_R1); }
+};
+
+// A-fragment of k-step ks of M tile m (lane layout of mfma 16x16x32: row col, k-group kgl)
+template <int I, typename T>
+__device__ __forceinline__ bf16x8_t ext_a(const ExtCtx<T>& c, int m, int ks) {
+    using S = ExtSpec<I>;
+    const T* w = (const T*)c.a->w[I];
+    if constexpr (S::PIPE) {
+        const int ch = ks / S::NTAP, tap = S::TLO + ks % S::NTAP;
+        return *(const bf16x8_t*)(w + S::WPIPE + ((m * S::NCH + ch) * 9 + tap) * 512 + c.lane * 8);
+    } else {
+        return *(const bf16x8_t*)(w + (m * 16 + c.col) * S::KP + (S::KS_LO + ks) * 32 + c.kgl * 8);
+    }
+}
+// physical cout of accumulator row 4*kgl + r of M tile m
+template <int I, typename T>
+__device__ __forceinline__ int ext_co(const ExtCtx<T>& c, int m) {
+    using S = ExtSpec<I>;
+    if constexpr (S::PIPE) {
+        constexpr int BPT = S::P / 16;
+        const int i = m % BPT;
+        return (m / BPT) * S::P + 32 * (i >> 1) + 8 * c.kgl + 4 * (i & 1);
+    } else {
+        return m * 16 + 4 * c.kgl;
+    }
+}
+template <int I, typename T>
+__device__ __forceinline__ void ext_bias(const ExtCtx<T>& c, int m, float (&b)[4]) {
+    using S = ExtSpec<I>;
+    const int co = ext_co<I>(c, m);
+    const float* bias = c.a->bias[I];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) b[r] = co + r < S::COUT ? bias[co + r] : 0.f;
+}
+// LDS offset of k-step ks's B-fragment from a pixel's window origin; live = the k-group is a real one
+template <int I, typename T>
+__device__ __forceinline__ int ext_boff(const ExtCtx<T>& c, int ks, bool& live) {
+    using S = ExtSpec<I>;
+    if constexpr (S::PIPE) {
+        const int ch = ks / S::NTAP, tap = S::TLO + ks % S::NTAP;
+        live = true;
+        return ((tap / 3) * S::IBW + tap % 3) * S::ILD + ch * 32 + c.kgl * 8;
+    } else {
+        const int kg = (S::KS_LO + ks) * 4 + c.kgl;
+        const int tap = kg / S::CG, cg = kg - tap * S::CG;
+        live = kg < 9 * S::CG;
+        return ((tap / 3) * S::IBW + tap % 3) * S::ILD + cg * 8;
+    }
+}
+
+template <int I, typename T>
+__device__ __forceinline__ void ext_prefetch(ExtCtx<T>& c) {
+    if constexpr (I < EXT_CONVS) {
+        using S = ExtSpec<I>;
+        const int m = c.wave % S::MT;
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+            c.pa[I % 2][j] = j < S::NKS ? ext_a<I>(c, m, j) : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+        ext_bias<I>(c, m, c.pb[I % 2]);
+    }
+}
+
+// One conv: barrier, prefetch of the next conv's fragments, border zeroing, the wave's items, epilogues.
+template <int I, typename T>
+__device__ __forceinline__ void ext_conv(ExtCtx<T>& c) {
+    using S = ExtSpec<I>;
+    const bf16x8_t zero8 = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+    __syncthreads();                      // the previous conv's output is complete; its input is consumed
+    EXT_STAMP(1 + 2 * I);
+    ext_prefetch<I + 1>(c);
+    const T* in = c.img(S::IN_BUF);
+    T* out = c.img(S::OUT_BUF);
+    {   // the output image's border, all channel slots: the buffer held another geometry before
+        constexpr int S8 = S::OLD / 8, NB = 2 * S::OBW + 2 * S::OH;
+        for (int i = threadIdx.x; i < NB * S8; i += 512) {
+            const int bp = i / S8, ch = i - bp * S8;
+            int y, x;
+            if (bp < S::OBW) { y = 0; x = bp; }
+            else if (bp < 2 * S::OBW) { y = S::OBW - 1; x = bp - S::OBW; }
+            else { const int r = bp - 2 * S::OBW; y = 1 + (r >> 1); x = (r & 1) ? S::OBW - 1 : 0; }
+            *(u32x4_t*)(out + (y * S::OBW + x) * S::OLD + ch * 8) = u32x4_t{0u, 0u, 0u, 0u};
+        }
+    }
+    auto origin = [&](int n) {            // window origin of this lane's pixel in N tile n (pad slots: pixel 0)
+        const int p = n * 16 + c.col;
+        const int oy = p < S::NPIX ? p / S::OH : 0, ox = p < S::NPIX ? p % S::OH : 0;
+        return in + ((oy * S::S) * S::IBW + ox * S::S) * S::ILD;
+    };
+    auto store = [&](const f32x4_t& acc, const float (&bias)[4], int m, int n) {
+        const int p = n * 16 + c.col;
+        if (p >= S::NPIX) return;
+        const int oy = p / S::OH, ox = p % S::OH;
+        const int co = ext_co<I>(c, m);
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float t = acc[r] + bias[r];
+            v[r] = t > 0.f ? t : 0.1f * t;
+        }
+        uint2 q;
+        q.x = H16<T>::pack(v[0], v[1]);
+        q.y = H16<T>::pack(v[2], v[3]);
+        *(uint2*)(out + ((oy + 1) * S::OBW + ox + 1) * S::OLD + co) = q;
+        if constexpr (S::J == 2) {
+            const dbsr_tensor& L = c.a->lv[S::L];
+            *(uint2*)(img_ptr<T>(L, c.f) + (long long)p * L.ld + co) = q;
+        }
+    };
+    // k-steps [k0, k1) with fragments from registers (A) or streamed from global memory (A == nullptr):
+    // batches of 4 (B reads, then MFMAs), one or two pixel tiles
+    auto mma = [&](const bf16x8_t* A, int m, int k0, int k1, const T* b1, const T* b2, f32x4_t& acc1,
+                   f32x4_t& acc2, bool two) {
+#pragma unroll
+        for (int j0 = k0; j0 < k1; j0 += 4) {
+            bf16x8_t Aq[4], B1[4], B2[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int ks = j0 + j < k1 ? j0 + j : k0;
+                Aq[j] = A ? A[ks] : ext_a<I>(c, m, ks);
+                bool live;
+                const int off = ext_boff<I>(c, ks, live);
+                B1[j] = live ? *(const bf16x8_t*)(b1 + off) : zero8;
+                B2[j] = (live && two) ? *(const bf16x8_t*)(b2 + off) : zero8;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (j0 + j < k1) {
+                    acc1 = mfma16<T>(Aq[j], B1[j], acc1);
+                    if (two) acc2 = mfma16<T>(Aq[j], B2[j], acc2);
+                }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+    constexpr int KH = S::NKS < 16 ? S::NKS : 16;        // k-steps held in the prefetched set
+    const bf16x8_t* A0 = c.pa[I % 2];
+    if constexpr (S::FIXED_M) {
+        // every item of this wave has M tile wave % MT; it walks its N tiles two at a time
+        constexpr int NSTEP = 8 / S::MT;
+        const int m = c.wave % S::MT;
+        for (int n = c.wave / S::MT; n < S::NT; n += 2 * NSTEP) {
+            const int n2 = n + NSTEP;
+            const bool two = n2 < S::NT;
+            const T* b1 = origin(n);
+            const T* b2 = origin(two ? n2 : n);
+            f32x4_t acc1 = f32x4_t{0.f, 0.f, 0.f, 0.f}, acc2 = acc1;
+            mma(A0, m, 0, KH, b1, b2, acc1, acc2, two);
+            if constexpr (S::NKS > 16) mma(nullptr, m, 16, S::NKS, b1, b2, acc1, acc2, two);
+            store(acc1, c.pb[I % 2], m, n);
+            if (two) store(acc2, c.pb[I % 2], m, n2);
+        }
+    } else {
+        // one N tile (the 4x4 and 1x1 levels): M tiles wave and wave + 8
+        static_assert(S::NT == 1 && S::MT <= 16, "general path: one pixel tile, <= 16 M tiles");
+        const T* b1 = origin(0);
+        if (c.wave < S::MT) {
+            f32x4_t acc1 = f32x4_t{0.f, 0.f, 0.f, 0.f}, acc2 = acc1;
+            mma(A0, c.wave, 0, KH, b1, b1, acc1, acc2, false);
+            if constexpr (S::NKS > 16) mma(nullptr, c.wave, 16, S::NKS, b1, b1, acc1, acc2, false);
+            store(acc1, c.pb[I % 2], c.wave, 0);
+        }
+        if (c.wave + 8 < S::MT) {
+            float bb[4];
+            ext_bias<I>(c, c.wave + 8, bb);
+            f32x4_t acc1 = f32x4_t{0.f, 0.f, 0.f, 0.f}, acc2 = acc1;
+            mma(nullptr, c.wave + 8, 0, S::NKS, b1, b1, acc1, acc2, false);
+            store(acc1, bb, c.wave + 8, 0);
+        }
+    }
+    EXT_STAMP(2 + 2 * I);
+}
+
+template <typename T, int... Is>
+__device__ __forceinline__ void ext_all(ExtCtx<T>& c, std::integer_sequence<int, Is...>) {
+    (ext_conv<Is>(c), ...);
+}
 
 template <typename T>
 __global__ __launch_bounds__(512) void pwc_extract_kernel(ExtArgs a) {
     __shared__ __attribute__((aligned(16))) u32x4_t smem[EXT_ELEMS / 8];
-    T* const base = (T*)smem;
-    const int f = blockIdx.x;
-    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int kgl = lane >> 4, col = lane & 15;
-
-    // the frame into image 0 (66x66, zero border)
-    {
-        const T* src = img_ptr<T>(a.rgb, f);
+    ExtCtx<T> c;
+    c.a = &a;
+    c.base = (T*)smem;
+    c.f = blockIdx.x;
+    c.lane = threadIdx.x & 63;
+    c.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    c.kgl = c.lane >> 4;
+    c.col = c.lane & 15;
+    EXT_STAMP(0);
+    ext_prefetch<0>(c);
+    {   // the frame into image 0 (66x66, zero border)
+        const T* src = img_ptr<T>(a.rgb, c.f);
         for (int i = threadIdx.x; i < 66 * 66; i += 512) {
             const int y = i / 66 - 1, x = i - (i / 66) * 66 - 1;
             u32x4_t v = u32x4_t{0u, 0u, 0u, 0u};
             if ((unsigned)y < 64u && (unsigned)x < 64u) v = *(const u32x4_t*)(src + (y * 64 + x) * a.rgb.ld);
-            *(u32x4_t*)(base + i * 8) = v;
+            *(u32x4_t*)(c.base + i * 8) = v;
         }
     }
-    auto img = [&](int b) { return base + (b == 0 ? 0 : b == 1 ? EXT_R0 : EXT_R0 + EXT_R1); };
-
-    for (int ci = 0; ci < EXT_CONVS; ++ci) {
-        __syncthreads();                  // the previous conv's output is complete; its input is consumed
-        const ExtConv& cv = a.cv[ci];
-        const T* in = img(cv.in_buf);
-        T* out = img(cv.out_buf);
-        const int obw = cv.ow + 2, obh = cv.oh + 2, ibw = cv.iw + 2;
-        // the output image's border (every channel slot) to zero: the buffer held another geometry before
-        {
-            const int s8 = cv.old / 8, nb = 2 * obw + 2 * cv.oh;
-            for (int i = threadIdx.x; i < nb * s8; i += 512) {
-                const int bp = i / s8, c = i - bp * s8;
-                int y, x;
-                if (bp < obw) { y = 0; x = bp; }
-                else if (bp < 2 * obw) { y = obh - 1; x = bp - obw; }
-                else { const int r = bp - 2 * obw; y = 1 + (r >> 1); x = (r & 1) ? obw - 1 : 0; }
-                *(u32x4_t*)(out + (y * obw + x) * cv.old + c * 8) = u32x4_t{0u, 0u, 0u, 0u};
-            }
-        }
-        const int npix = cv.oh * cv.ow;
-        const int ntiles = (npix + 15) / 16;
-        const int items = cv.mt * ntiles;
-        const int nks = cv.ks_hi - cv.ks_lo;
-        // epilogue of one (M tile m, N tile n) accumulator: lane (kgl, col) holds couts m*16 + 4*kgl .. +3 of
-        // pixel n*16 + col
-        auto store = [&](const f32x4_t& acc, int m, int n) {
-            const int p = n * 16 + col;
-            if (p >= npix) return;
-            const int oy = p / cv.ow, ox = p - (p / cv.ow) * cv.ow;
-            const int co = m * 16 + 4 * kgl;
-            float v[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float b = (cv.bias && co + r < cv.cout) ? cv.bias[co + r] : 0.f;
-                const float t = acc[r] + b;
-                v[r] = t > 0.f ? t : 0.1f * t;
-            }
-            uint2 q;
-            q.x = H16<T>::pack(v[0], v[1]);
-            q.y = H16<T>::pack(v[2], v[3]);
-            *(uint2*)(out + ((oy + 1) * obw + ox + 1) * cv.old + co) = q;
-            if (cv.level >= 0) {
-                const dbsr_tensor& L = a.lv[cv.level];
-                *(uint2*)(img_ptr<T>(L, f) + (long long)p * L.ld + co) = q;
-            }
-        };
-        // the LDS offset of k-step j's B-fragment relative to a pixel's window origin (tap-major k-groups)
-        auto b_off = [&](int j, bool& ok) {
-            const int kg = (cv.ks_lo + j) * 4 + kgl;
-            const int tap = kg / cv.CG, cg = kg - tap * cv.CG;
-            ok = kg < cv.KG;
-            const int ky = tap / 3, kx = tap - (tap / 3) * 3;
-            return (ky * ibw + kx) * cv.ild + cg * 8;
-        };
-        auto origin = [&](int n) {          // window origin of this lane's pixel in tile n (pad slots: pixel 0)
-            const int p = n * 16 + col;
-            const int oy = p < npix ? p / cv.ow : 0, ox = p < npix ? p - (p / cv.ow) * cv.ow : 0;
-            return in + ((oy * cv.stride) * ibw + ox * cv.stride) * cv.ild;
-        };
-        if (8 % cv.mt == 0 && nks <= 16) {
-            // every item of this wave has M tile wave % mt: its A-fragments and B offsets load once, then the
-            // wave walks its N tiles two at a time (two independent MFMA chains)
-            const int m = wave % cv.mt, nstep = 8 / cv.mt;
-            const T* wrow = (const T*)cv.w + (long long)(m * 16 + col) * cv.Kp + kgl * 8;
-            bf16x8_t A[16];
-            int bo[16];
-            bool bv[16];
-#pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                A[j] = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
-                bv[j] = false;
-                bo[j] = 0;
-                if (j < nks) {
-                    A[j] = *(const bf16x8_t*)(wrow + (cv.ks_lo + j) * 32);
-                    bo[j] = b_off(j, bv[j]);
-                }
-            }
-            for (int n = wave / cv.mt; n < ntiles; n += 2 * nstep) {
-                const int n2 = n + nstep;
-                const T* b1 = origin(n);
-                const T* b2 = origin(n2 < ntiles ? n2 : n);
-                f32x4_t acc1 = f32x4_t{0.f, 0.f, 0.f, 0.f}, acc2 = acc1;
-#pragma unroll
-                for (int j = 0; j < 16; ++j) {
-                    if (j < nks) {
-                        const bf16x8_t z = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
-                        const bf16x8_t B1 = bv[j] ? *(const bf16x8_t*)(b1 + bo[j]) : z;
-                        const bf16x8_t B2 = bv[j] ? *(const bf16x8_t*)(b2 + bo[j]) : z;
-                        acc1 = mfma16<T>(A[j], B1, acc1);
-                        acc2 = mfma16<T>(A[j], B2, acc2);
-                    }
-                }
-                store(acc1, m, n);
-                if (n2 < ntiles) store(acc2, m, n2);
-            }
-            continue;
-        }
-        for (int it = wave; it < items; it += 8) {
-            const int m = it % cv.mt, n = it / cv.mt;
-            const T* bin = origin(n);
-            const T* wrow = (const T*)cv.w + (long long)(m * 16 + col) * cv.Kp + kgl * 8;
-            f32x4_t acc = f32x4_t{0.f, 0.f, 0.f, 0.f};
-            for (int k0 = 0; k0 < nks; k0 += 8) {
-                bf16x8_t A[8], B[8];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const bool ok = k0 + j < nks;
-                    A[j] = *(const bf16x8_t*)(wrow + (cv.ks_lo + (ok ? k0 + j : 0)) * 32);
-                    bool live;
-                    const int off = b_off(ok ? k0 + j : 0, live);
-                    B[j] = (ok && live) ? *(const bf16x8_t*)(bin + off) : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
-                }
-#pragma unroll
-                for (int j = 0; j < 8; ++j)
-                    if (k0 + j < nks) acc = mfma16<T>(A[j], B[j], acc);
-            }
-            store(acc, m, n);
-        }
-    }
+    ext_all<T>(c, std::make_integer_sequence<int, EXT_CONVS>{});
+    EXT_STAMP(39);
 }
 
 }  // namespace
+
+#ifdef DBSR_EXT_STAMPS
+extern "C" int dbsr_diag_ext_stamps(unsigned long long* host, long long n) {
+    if (!host) {
+        static unsigned long long z[128 * 8 * 40];
+        return hipMemcpyToSymbol(HIP_SYMBOL(g_ext_stamps), z, sizeof(z)) == hipSuccess ? 0 : -1;
+    }
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ext_stamps), n * 8) == hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" int dbsr_pwc_extract_supported(int Hp, int Wp) { return Hp == 64 && Wp == 64 ? 1 : 0; }
 
 extern "C" int dbsr_pwc_extract(int F, int Hp, int Wp, dbsr_tensor rgb, const dbsr_pwc_ext_conv* convs,
                                 const dbsr_tensor* levels, void* stream) {
-    static const int CH[7] = {3, 16, 32, 64, 96, 128, 196};    // pwcnet.py:49-100
     DBSR_CHECK_ARG(convs && levels && rgb.ptr && rgb.map.fpg > 0, "pwc_extract: null argument");
     DBSR_CHECK_ARG(dbsr_pwc_extract_supported(Hp, Wp), "pwc_extract: needs a 64x64 frame (got %dx%d)", Hp, Wp);
     DBSR_CHECK_ARG(rgb.dtype == DBSR_BF16 || rgb.dtype == DBSR_F16, "pwc_extract: 16-bit activations only");
@@ -222,54 +341,20 @@ extern "C" int dbsr_pwc_extract(int F, int Hp, int Wp, dbsr_tensor rgb, const db
     ExtArgs a;
     a.F = F;
     a.rgb = rgb;
-    int in_buf = 0, ih = 64;
     for (int l = 0; l < 6; ++l) {
         const dbsr_tensor& L = levels[l];
-        DBSR_CHECK_ARG(L.ptr && L.dtype == rgb.dtype && L.map.fpg > 0 && L.c0 == 0 && L.ld == cpad_i(CH[l + 1]),
-                       "pwc_extract: level %d output must be a %d-channel slice of ld %d", l + 1, CH[l + 1],
-                       cpad_i(CH[l + 1]));
+        const int C = ext_ch(l + 1);
+        DBSR_CHECK_ARG(L.ptr && L.dtype == rgb.dtype && L.map.fpg > 0 && L.c0 == 0 && L.ld == cpad_c(C),
+                       "pwc_extract: level %d output must be a %d-channel slice of ld %d", l + 1, C, cpad_c(C));
         a.lv[l] = L;
         for (int j = 0; j < 3; ++j) {
             const int i = 3 * l + j;
-            const dbsr_pwc_ext_conv& c = convs[i];
-            const int cin = j == 0 ? CH[l] : CH[l + 1], cout = CH[l + 1], s = j == 0 ? 2 : 1;
-            DBSR_CHECK_ARG(c.w && c.cin == cin && c.cout == cout && c.stride == s,
-                           "pwc_extract: conv %d must be %d -> %d, stride %d", i, cin, cout, s);
-            ExtConv& e = a.cv[i];
-            e.w = c.w;
-            e.bias = c.bias;
-            e.CG = cpad_i(cin) / 8;
-            e.KG = 9 * e.CG;
-            e.Kp = round_up_i(e.KG, 4) * 8;
-            e.mt = cpad_i(cout) / 16;
-            e.cout = cout;
-            e.stride = s;
-            e.ih = e.iw = ih;
-            e.oh = e.ow = (ih + 2 - 3) / s + 1;
-            e.ild = i == 0 ? 8 : lds_ld(cin);
-            e.old = lds_ld(cout);
-            // taps with an in-frame input pixel for some output pixel (pad 1)
-            int tlo = 9, thi = -1;
-            for (int ky = 0; ky < 3; ++ky)
-                for (int kx = 0; kx < 3; ++kx) {
-                    bool yok = false, xok = false;
-                    for (int o = 0; o < e.oh; ++o) yok |= (unsigned)(o * s - 1 + ky) < (unsigned)ih;
-                    for (int o = 0; o < e.ow; ++o) xok |= (unsigned)(o * s - 1 + kx) < (unsigned)ih;
-                    if (yok && xok) {
-                        tlo = std::min(tlo, ky * 3 + kx);
-                        thi = std::max(thi, ky * 3 + kx);
-                    }
-                }
-            e.ks_lo = (tlo * e.CG) / 4;
-            e.ks_hi = std::min(((thi + 1) * e.CG + 3) / 4, e.Kp / 32);
-            e.in_buf = in_buf;
-            e.out_buf = in_buf == 1 ? 2 : 1;
-            e.level = j == 2 ? l : -1;
-            const int cap = e.out_buf == 0 ? EXT_R0 : EXT_R1;
-            DBSR_CHECK_ARG((e.oh + 2) * (e.ow + 2) * e.old <= cap, "pwc_extract: level %d image exceeds its LDS buffer",
-                           l + 1);
-            in_buf = e.out_buf;
-            ih = e.oh;
+            const dbsr_pwc_ext_conv& cv = convs[i];
+            const int cin = j == 0 ? ext_ch(l) : C, s = j == 0 ? 2 : 1;
+            DBSR_CHECK_ARG(cv.w && cv.bias && cv.cin == cin && cv.cout == C && cv.stride == s,
+                           "pwc_extract: conv %d must be %d -> %d, stride %d, with a bias", i, cin, C, s);
+            a.w[i] = cv.w;
+            a.bias[i] = cv.bias;
         }
     }
     hipStream_t s = (hipStream_t)stream;
