@@ -220,6 +220,235 @@ __global__ __launch_bounds__(512) void pwc_dense_kernel(DenseArgs a) {
     }
 }
 
+
+// ------------------------------------------------------------------------------------------------
+// The same DenseNet specialised per coarse level of the 64x64 pyramid (levels 6..3: 1x1 .. 8x8 pixels per
+// pair): every conv's geometry is a compile-time constant, so the k-loops unroll and the index math folds
+// (the run-time kernel above spends most of its time in loop and address overhead), and each wave loads the
+// first 16 A-fragments of its next conv right after the current conv's barrier so they arrive while it runs.
+// ------------------------------------------------------------------------------------------------
+__host__ __device__ constexpr int dcpad(int c) { return (c + 31) / 32 * 32; }
+__host__ __device__ constexpr int dense_out(int i) { return i == 0 ? 128 : i == 1 ? 128 : i == 2 ? 96 : i == 3 ? 64 : 32; }
+__host__ __device__ constexpr int dense_off(int i) { return i == 0 ? 320 : i == 1 ? 192 : i == 2 ? 96 : i == 3 ? 32 : 0; }
+
+template <int LEVEL> struct DenseLevel {
+    static constexpr int H = LEVEL == 6 ? 1 : LEVEL == 5 ? 2 : LEVEL == 4 ? 4 : 8;
+    static constexpr int C = LEVEL == 6 ? 196 : LEVEL == 5 ? 128 : LEVEL == 4 ? 96 : 64;
+    static constexpr int BASE = LEVEL == 6 ? 81 : 81 + C + 4;
+    static constexpr int LD = 448 + dcpad(BASE), LDS_LD = LD + 8;
+    static constexpr int HW = H * H, BW = H + 2, BHW = BW * BW;
+    static constexpr int PPB = HW == 1 ? 8 : (16 / HW > 1 ? 16 / HW : 1);
+    static constexpr int NT = (PPB * HW + 15) / 16;
+    static constexpr bool SINGLE = HW == 1;
+    static_assert(NT == 1 || NT == 4, "tile");
+    static_assert(PPB * BHW * LDS_LD <= DenseTile<NT>::ELEMS, "LDS tile");
+};
+template <int LEVEL, int I> struct DenseConvSpec {
+    using Lv = DenseLevel<LEVEL>;
+    static constexpr int CIN = I == 5 ? Lv::BASE + 448 : Lv::BASE + (I > 0 ? 128 : 0) + (I > 1 ? 128 : 0) +
+                                                           (I > 2 ? 96 : 0) + (I > 3 ? 64 : 0);
+    static constexpr int START = I == 5 ? 0 : I == 0 ? 448 : dense_off(I - 1);
+    static constexpr int COUT = I == 5 ? 2 : dense_out(I), OUT_OFF = I == 5 ? 0 : dense_off(I);
+    static constexpr int GPT = dcpad(CIN) / 32;                 // k-steps (32-channel chunks) per tap
+    static constexpr int NKS = Lv::SINGLE ? GPT : 9 * GPT;
+    static constexpr int MB = (COUT + 15) / 16;
+    static constexpr int KSPLIT = MB >= 5 ? 1 : MB >= 3 ? 2 : MB == 2 ? 4 : 8;
+    static constexpr int KPW = (NKS + KSPLIT - 1) / KSPLIT;     // k-steps per wave (upper bound)
+};
+
+template <typename T, int NT> struct DenseCtx {
+    T* tile;
+    const DenseArgs* a;
+    int lane, wave, g, col, np, pair0;
+    int base[NT];
+    bf16x8_t pa[2][16];
+};
+
+template <int LEVEL, int I, typename T, int NT>
+__device__ __forceinline__ const T* dense_wrow(const DenseCtx<T, NT>& c) {
+    using S = DenseConvSpec<LEVEL, I>;
+    const int m0 = c.wave / S::KSPLIT;
+    return (const T*)c.a->cv[I].w_pipe + (long long)(m0 < S::MB ? m0 : 0) * S::GPT * 9 * 512 + c.lane * 8;
+}
+// packed piece of this wave's k-step j (relative to its K slice) of conv I
+template <int LEVEL, int I>
+__device__ __forceinline__ int dense_piece(int kid, int j) {
+    using S = DenseConvSpec<LEVEL, I>;
+    int ks = kid * S::KPW + j;
+    ks = ks < S::NKS ? ks : S::NKS - 1;
+    return DenseLevel<LEVEL>::SINGLE ? ks * 9 + 4 : ks;
+}
+template <int LEVEL, int I, typename T, int NT>
+__device__ __forceinline__ void dense_prefetch(DenseCtx<T, NT>& c) {
+    if constexpr (I < 6) {
+        using S = DenseConvSpec<LEVEL, I>;
+        const T* w = dense_wrow<LEVEL, I>(c);
+        const int kid = c.wave % S::KSPLIT;
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+            c.pa[I % 2][j] = j < S::KPW ? *(const bf16x8_t*)(w + dense_piece<LEVEL, I>(kid, j) * 512)
+                                       : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+}
+
+template <int LEVEL, int I, typename T, int NT>
+__device__ __forceinline__ void dense_conv(DenseCtx<T, NT>& c, f32x4_t* red) {
+    using S = DenseConvSpec<LEVEL, I>;
+    using Lv = DenseLevel<LEVEL>;
+    __syncthreads();                                   // the previous conv's outputs are in the tile
+    dense_prefetch<LEVEL, I + 1>(c);
+    const int m0 = c.wave / S::KSPLIT, kid = c.wave % S::KSPLIT;
+    const bool active = m0 < S::MB;
+    f32x4_t acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    if (active) {
+        const T* w = dense_wrow<LEVEL, I>(c);
+        const int k_lo = kid * S::KPW;
+        auto b_at = [&](int j, int t) {                // B-fragment of the wave's k-step j, column tile t
+            int ks = k_lo + j;
+            ks = ks < S::NKS ? ks : S::NKS - 1;
+            const int ch = Lv::SINGLE ? ks : ks / 9, tap = Lv::SINGLE ? 4 : ks % 9;
+            const int off = ((tap / 3) * Lv::BW + tap % 3) * Lv::LDS_LD + S::START + ch * 32;
+            return *(const bf16x8_t*)(c.tile + c.base[t] + off);
+        };
+        const int nj = k_lo + S::KPW <= S::NKS ? S::KPW : S::NKS - k_lo;   // this wave's k-steps (wave-uniform)
+        constexpr int KH = S::KPW < 16 ? S::KPW : 16;
+#pragma unroll
+        for (int j0 = 0; j0 < KH; j0 += 4) {
+            bf16x8_t B[4][NT];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int t = 0; t < NT; ++t) B[j][t] = b_at(j0 + j, t);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (j0 + j < KH && j0 + j < nj) {
+#pragma unroll
+                    for (int t = 0; t < NT; ++t) acc[t] = mma16x16x32<T>(c.pa[I % 2][j0 + j], B[j][t], acc[t]);
+                }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int j0 = 16; j0 < S::KPW; j0 += 4) {
+            bf16x8_t A[4], B[4][NT];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                A[j] = *(const bf16x8_t*)(w + dense_piece<LEVEL, I>(kid, j0 + j < S::KPW ? j0 + j : j0) * 512);
+#pragma unroll
+                for (int t = 0; t < NT; ++t) B[j][t] = b_at(j0 + j, t);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (j0 + j < S::KPW && j0 + j < nj) {
+#pragma unroll
+                    for (int t = 0; t < NT; ++t) acc[t] = mma16x16x32<T>(A[j], B[j][t], acc[t]);
+                }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (S::KSPLIT > 1) {
+            if (kid > 0) {
+#pragma unroll
+                for (int t = 0; t < NT; ++t) red[(((kid - 1) * S::MB + m0) * NT + t) * 64 + c.lane] = acc[t];
+            }
+        }
+    }
+    if constexpr (S::KSPLIT > 1) __syncthreads();
+    if (active && kid == 0) {
+        if constexpr (S::KSPLIT > 1) {
+#pragma unroll
+            for (int k2 = 1; k2 < S::KSPLIT; ++k2)
+#pragma unroll
+                for (int t = 0; t < NT; ++t) acc[t] += red[(((k2 - 1) * S::MB + m0) * NT + t) * 64 + c.lane];
+        }
+        const DenseConv& cv = c.a->cv[I];
+        // MFMA row 4g + r of block m0 is cout 32(m0 >> 1) + 8g + 4(m0 & 1) + r (pipe_cout_perm)
+        const int co0 = 32 * (m0 >> 1) + 8 * c.g + 4 * (m0 & 1);
+        float bias[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bias[r] = (cv.bias && co0 + r < S::COUT) ? cv.bias[co0 + r] : 0.f;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int slot = t * 16 + c.col;
+            if (slot >= c.np) continue;
+            const int pl = slot / Lv::HW, px = slot % Lv::HW, y = px / Lv::H, x = px % Lv::H;
+            const int row = pl * Lv::BHW + (y + 1) * Lv::BW + x + 1;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                if (co0 + r >= S::COUT) continue;
+                const float v = acc[t][r] + bias[r];
+                if constexpr (I < 5) {
+                    elem<T>::st(c.tile + row * Lv::LDS_LD + S::OUT_OFF + co0 + r, v > 0.f ? v : 0.1f * v);
+                } else {
+                    const DenseArgs& a = *c.a;
+                    float* fo = (float*)a.flow.ptr + map_frame(a.flow.map, c.pair0 + pl) * a.flow.img_stride +
+                                (long long)px * a.flow.ld + a.flow.c0 + co0 + r;
+                    *fo = v;
+                }
+            }
+        }
+    }
+}
+
+template <typename T, int LEVEL>
+__global__ __launch_bounds__(512) void pwc_dense_level_kernel(DenseArgs a) {
+    using Lv = DenseLevel<LEVEL>;
+    constexpr int NT = Lv::NT;
+    __shared__ __attribute__((aligned(16))) u32x4_t smem[DenseTile<NT>::ELEMS / 8];
+    __shared__ f32x4_t red[7 * NT * 64];
+    DenseCtx<T, NT> c;
+    c.tile = (T*)smem;
+    c.a = &a;
+    c.lane = threadIdx.x & 63;
+    c.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    c.g = c.lane >> 4;
+    c.col = c.lane & 15;
+    c.pair0 = blockIdx.x * Lv::PPB;
+    const int npairs = min(Lv::PPB, a.P - c.pair0);
+    c.np = npairs * Lv::HW;
+    constexpr int C8 = Lv::LD / 8, L8 = Lv::LDS_LD / 8;
+    dense_prefetch<LEVEL, 0>(c);
+    for (int i = threadIdx.x; i < npairs * Lv::BHW * L8; i += 512)
+        *(u32x4_t*)(c.tile + i * 8) = u32x4_t{0u, 0u, 0u, 0u};
+    __syncthreads();
+    for (int i = threadIdx.x; i < c.np * C8; i += 512) {
+        const int slot = i / C8, ch = i % C8;
+        const int pl = slot / Lv::HW, px = slot % Lv::HW, y = px / Lv::H, x = px % Lv::H;
+        *(u32x4_t*)(c.tile + (pl * Lv::BHW + (y + 1) * Lv::BW + x + 1) * Lv::LDS_LD + ch * 8) =
+            *(const u32x4_t*)(img_ptr<T>(a.D, c.pair0 + pl) + (long long)px * a.D.ld + ch * 8);
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const int slot = t * 16 + c.col;
+        const int pl = slot / Lv::HW, px = slot % Lv::HW, y = px / Lv::H, x = px % Lv::H;
+        c.base[t] = (slot < c.np ? (pl * Lv::BHW + y * Lv::BW + x) * Lv::LDS_LD : 0) + c.g * 8;
+    }
+    dense_conv<LEVEL, 0>(c, red);
+    dense_conv<LEVEL, 1>(c, red);
+    dense_conv<LEVEL, 2>(c, red);
+    dense_conv<LEVEL, 3>(c, red);
+    dense_conv<LEVEL, 4>(c, red);
+    dense_conv<LEVEL, 5>(c, red);
+    __syncthreads();
+    // dense channels back to global D (read by the next level's upfeat ConvT)
+    const int d8 = a.dense_ch / 8;
+    for (int i = threadIdx.x; i < c.np * d8; i += 512) {
+        const int slot = i / d8, ch = i % d8;
+        const int pl = slot / Lv::HW, px = slot % Lv::HW, y = px / Lv::H, x = px % Lv::H;
+        *(u32x4_t*)(img_ptr<T>(a.D, c.pair0 + pl) + (long long)px * a.D.ld + ch * 8) =
+            *(const u32x4_t*)(c.tile + (pl * Lv::BHW + (y + 1) * Lv::BW + x + 1) * Lv::LDS_LD + ch * 8);
+    }
+}
+
+// the specialised level (6..3) for an h x h level with ld channels in D, 0 if none
+int dense_level_of(int h, int w, int ld) {
+    if (h != w) return 0;
+    if (h == DenseLevel<6>::H && ld == DenseLevel<6>::LD) return 6;
+    if (h == DenseLevel<5>::H && ld == DenseLevel<5>::LD) return 5;
+    if (h == DenseLevel<4>::H && ld == DenseLevel<4>::LD) return 4;
+    if (h == DenseLevel<3>::H && ld == DenseLevel<3>::LD) return 3;
+    return 0;
+}
 }  // namespace
 
 #ifdef DBSR_PIPE_STAMPS
@@ -265,12 +494,41 @@ extern "C" int dbsr_pwc_dense(int P, int h, int w, dbsr_tensor D, int dense_ch, 
         a.cv[i] = DenseConv{wp, c.bias, c.kp, c.cg, c.start, c.cout, c.out_off};
     }
     const int hw = h * w;
+    hipStream_t s = (hipStream_t)stream;
+    if (const int lvl = dense_level_of(h, w, D.ld)) {
+        // the conv list must be the level's DenseNet (pwcnet.py:123-150) for the specialised kernel
+        bool std_convs = true;
+        const int base = lvl == 6 ? 81 : 81 + (lvl == 5 ? 128 : lvl == 4 ? 96 : 64) + 4;
+        int cin = base;
+        for (int i = 0; i < 6; ++i) {
+            const int start = i == 5 ? 0 : i == 0 ? 448 : dense_off(i - 1);
+            const int cout = i == 5 ? 2 : dense_out(i);
+            std_convs = std_convs && convs[i].cg * 8 == dcpad(i == 5 ? base + 448 : cin) && convs[i].start == start &&
+                        convs[i].cout == cout && (i == 5 || convs[i].out_off == dense_off(i));
+            if (i < 5) cin += cout;
+        }
+        if (std_convs && dense_ch == 448) {
+            const int ppb = lvl == 6 ? 8 : lvl == 5 ? 4 : 1;
+            a.ppb = ppb;
+            const unsigned grid = (unsigned)((P + ppb - 1) / ppb);
+#define DBSR_DENSE_LVL(L)                                                                                 \
+    if (lvl == L) {                                                                                      \
+        if (D.dtype == DBSR_BF16)                                                                        \
+            hipLaunchKernelGGL((pwc_dense_level_kernel<bf16_t, L>), dim3(grid), dim3(512), 0, s, a);     \
+        else                                                                                             \
+            hipLaunchKernelGGL((pwc_dense_level_kernel<f16_t, L>), dim3(grid), dim3(512), 0, s, a);      \
+    }
+            DBSR_DENSE_LVL(6) DBSR_DENSE_LVL(5) DBSR_DENSE_LVL(4) DBSR_DENSE_LVL(3)
+#undef DBSR_DENSE_LVL
+            DBSR_LAUNCH_CHECK();
+            return 0;
+        }
+    }
     DBSR_CHECK_ARG(dense_fits(h, w, D.ld), "pwc_dense: no LDS tile for %dx%d pixels x %d channels "
                    "(dbsr_pwc_dense_supported)", h, w, D.ld);
     a.ppb = dense_ppb(h, w);             // one 16-slot column tile of pairs, or one pair of 64 pixels
     const int nt = (a.ppb * hw + 15) / 16;
     const unsigned grid = (unsigned)((P + a.ppb - 1) / a.ppb);
-    hipStream_t s = (hipStream_t)stream;
 #define DBSR_DENSE(T, NT) \
     hipLaunchKernelGGL((pwc_dense_kernel<T, NT>), dim3(grid), dim3(512), 0, s, a)
     if (D.dtype == DBSR_BF16) {

@@ -425,31 +425,34 @@ __device__ __forceinline__ void convt_px(const PrepArgs& a, const dbsr_tensor& i
     }
 }
 
-template <typename T>
+// Specialised per level (H x H pixels, C channels; PREV: a previous level exists) so every loop bound and
+// index is a compile-time constant.
+template <typename T, int H, int C, bool PREV>
 __global__ __launch_bounds__(256) void pwc_level_prep_kernel(PrepArgs a) {
+    constexpr int W = H, NPIX = H * W, CP = cpad_c(C), C8 = CP / 8, BW = W + 8, BH = H + 8;
     __shared__ __attribute__((aligned(16))) unsigned char smem[PREP_LDS_BYTES];
-    const int pair = blockIdx.x, h = a.h, w = a.w, npix = h * w, Cp = a.Cp, c8 = Cp / 8;
-    const int bw = w + 8, bh = h + 8;
-    float* up = (float*)smem;                          // [npix][4]: upflow x, y, upfeat 0, 1
-    T* fst = (T*)(smem + npix * 16);                   // [npix][Cp]
-    T* wrp = fst + npix * Cp;                          // [(h+8) x (w+8)][Cp], 4-pixel zero border
+    static_assert(NPIX * 16 + NPIX * CP * 2 + BH * BW * CP * 2 <= PREP_LDS_BYTES, "level tile exceeds the LDS");
+    const int pair = blockIdx.x;
+    float* up = (float*)smem;                          // [NPIX][4]: upflow x, y, upfeat 0, 1
+    T* fst = (T*)(smem + NPIX * 16);                   // [NPIX][CP]
+    T* wrp = fst + NPIX * CP;                          // [(H+8) x (W+8)][CP], 4-pixel zero border
     const int t = threadIdx.x;
+    const int lane = t & 63, wave = t >> 6, kgl = lane >> 4, col = lane & 15;
 
     // ---- upflow / upfeat (ConvTranspose2d k4 s2 p1) of the previous level ----
     // upfeat: every (tap, cout) contribution of every previous-level pixel as one small GEMM on MFMA,
     // part[in_px][(ky*4+kx)*2+co] = sum_ci D_prev[in_px][ci] * w[ky][kx][co][ci] (M = 32 rows, N = the previous
     // level's pixels, K = its channels), then each output pixel sums its <= 4 (input pixel, tap) terms.  The
     // 2-channel upflow keeps the scalar form (convt_k4s2_kernel's arithmetic).
-    float* part = (float*)(smem + npix * 16);         // [npix / 4][32] (before the first-feature image exists)
-    if (a.has_prev) {
-        const int pw = w / 2, pnp = npix / 4;
-        const int lane = t & 63, wave = t >> 6, kgl = lane >> 4, col = lane & 15;
-        const int ntn = (pnp + 15) / 16, nks = a.pcin32 / 32;
+    if constexpr (PREV) {
+        constexpr int PW = W / 2, PNP = NPIX / 4, NTN = (PNP + 15) / 16;
+        float* part = (float*)(smem + NPIX * 16);     // [PNP][32] (before the first-feature image exists)
+        const int nks = a.pcin32 / 32;
         const T* pd = img_ptr<T>(a.pD, pair);
-        for (int item = wave; item < 2 * ntn; item += 4) {
+        for (int item = wave; item < 2 * NTN; item += 4) {
             const int mt = item & 1, nt = item >> 1;
             const int q = nt * 16 + col;
-            const T* brow = pd + (long long)(q < pnp ? q : 0) * a.pD.ld + kgl * 8;
+            const T* brow = pd + (long long)(q < PNP ? q : 0) * a.pD.ld + kgl * 8;
             const T* arow = (const T*)a.wfeat + (long long)(mt * 16 + col) * a.pcin32 + kgl * 8;
             f32x4_t acc = f32x4_t{0.f, 0.f, 0.f, 0.f};
             for (int k0 = 0; k0 < nks; k0 += 8) {
@@ -464,25 +467,27 @@ __global__ __launch_bounds__(256) void pwc_level_prep_kernel(PrepArgs a) {
                 for (int j = 0; j < 8; ++j)
                     if (k0 + j < nks) acc = mfma16<T>(A[j], B[j], acc);
             }
-            if (q < pnp) {
+            if (q < PNP) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) part[q * 32 + mt * 16 + 4 * kgl + r] = acc[r];
             }
         }
         __syncthreads();
-        for (int q = t; q < npix; q += 256) {
-            const int oy = q / w, ox = q - (q / w) * w;
+        for (int q = t; q < NPIX; q += 256) {
+            const int oy = q / W, ox = q % W;
             float af[2];
             convt_px<float>(a, a.pflow, pair, 8, a.wflow, oy, ox, 0, 1, af);
             float ad0 = 0.f, ad1 = 0.f;
             const int ky0 = (oy + 1) & 1, kx0 = (ox + 1) & 1;
+#pragma unroll
             for (int aa = 0; aa < 2; ++aa) {
                 const int ky = ky0 + 2 * aa, iy = (oy + 1 - ky) >> 1;
-                if (iy < 0 || iy >= h / 2) continue;
+                if (iy < 0 || iy >= H / 2) continue;
+#pragma unroll
                 for (int bq = 0; bq < 2; ++bq) {
                     const int kx = kx0 + 2 * bq, ix = (ox + 1 - kx) >> 1;
-                    if (ix < 0 || ix >= pw) continue;
-                    const float* pp = part + (iy * pw + ix) * 32 + (ky * 4 + kx) * 2;
+                    if (ix < 0 || ix >= PW) continue;
+                    const float* pp = part + (iy * PW + ix) * 32 + (ky * 4 + kx) * 2;
                     ad0 += pp[0];
                     ad1 += pp[1];
                 }
@@ -497,48 +502,48 @@ __global__ __launch_bounds__(256) void pwc_level_prep_kernel(PrepArgs a) {
     // ---- first features into the LDS; the warped image's border to zero ----
     {
         const T* f1 = img_ptr<T>(a.first, pair);
-        for (int i = t; i < npix * c8; i += 256) {
-            const int q = i / c8, c = i - q * c8;
-            *(u32x4_t*)(fst + q * Cp + c * 8) = *(const u32x4_t*)(f1 + (long long)q * a.first.ld + c * 8);
+        for (int i = t; i < NPIX * C8; i += 256) {
+            const int q = i / C8, c = i % C8;
+            *(u32x4_t*)(fst + q * CP + c * 8) = *(const u32x4_t*)(f1 + (long long)q * a.first.ld + c * 8);
         }
-        for (int i = t; i < bh * bw * c8; i += 256) {
-            const int q = i / c8, c = i - q * c8;
-            const int y = q / bw - 4, x = q - (q / bw) * bw - 4;
-            if ((unsigned)y >= (unsigned)h || (unsigned)x >= (unsigned)w)
-                *(u32x4_t*)(wrp + q * Cp + c * 8) = u32x4_t{0u, 0u, 0u, 0u};
+        for (int i = t; i < BH * BW * C8; i += 256) {
+            const int q = i / C8, c = i % C8;
+            const int y = q / BW - 4, x = q % BW - 4;
+            if ((unsigned)y >= (unsigned)H || (unsigned)x >= (unsigned)W)
+                *(u32x4_t*)(wrp + q * CP + c * 8) = u32x4_t{0u, 0u, 0u, 0u};
         }
     }
     __syncthreads();                                   // upflow ready
     // ---- backwarp of the second features (backwarp_kernel's arithmetic) into the bordered image ----
     {
         const T* sb = img_ptr<T>(a.second, pair);
-        for (int i = t; i < npix * c8; i += 256) {
-            const int q = i / c8, g = i - q * c8;
-            const int y = q / w, x = q - (q / w) * w;
+        for (int i = t; i < NPIX * C8; i += 256) {
+            const int q = i / C8, g = i % C8;
+            const int y = q / W, x = q % W;
             float v[8];
-            if (!a.has_prev) {
+            if constexpr (!PREV) {
                 load8(sb + (long long)q * a.second.ld + g * 8, v);
             } else {
                 const float fx = up[q * 4 + 0] * a.scale, fy = up[q * 4 + 1] * a.scale;
-                const float gxn = (-1.0f + (2.0f * x + 1.0f) / (float)w) + fx / (((float)w - 1.0f) / 2.0f);
-                const float gyn = (-1.0f + (2.0f * y + 1.0f) / (float)h) + fy / (((float)h - 1.0f) / 2.0f);
-                const float ix = ((gxn + 1.f) * (float)w - 1.f) / 2.f;
-                const float iy = ((gyn + 1.f) * (float)h - 1.f) / 2.f;
+                const float gxn = (-1.0f + (2.0f * x + 1.0f) / (float)W) + fx / (((float)W - 1.0f) / 2.0f);
+                const float gyn = (-1.0f + (2.0f * y + 1.0f) / (float)H) + fy / (((float)H - 1.0f) / 2.0f);
+                const float ix = ((gxn + 1.f) * (float)W - 1.f) / 2.f;
+                const float iy = ((gyn + 1.f) * (float)H - 1.f) / 2.f;
                 const float fx0 = floorf(ix), fy0 = floorf(iy);
                 const int x0 = (int)fx0, y0 = (int)fy0, x1 = x0 + 1, y1 = y0 + 1;
                 const float wx1 = ix - fx0, wx0 = 1.f - wx1, wy1 = iy - fy0, wy0 = 1.f - wy1;
-                const bool vx0 = (unsigned)x0 < (unsigned)w, vx1 = (unsigned)x1 < (unsigned)w;
-                const bool vy0 = (unsigned)y0 < (unsigned)h, vy1 = (unsigned)y1 < (unsigned)h;
+                const bool vx0 = (unsigned)x0 < (unsigned)W, vx1 = (unsigned)x1 < (unsigned)W;
+                const bool vy0 = (unsigned)y0 < (unsigned)H, vy1 = (unsigned)y1 < (unsigned)H;
                 const float w00 = (vy0 && vx0) ? wy0 * wx0 : 0.f, w01 = (vy0 && vx1) ? wy0 * wx1 : 0.f;
                 const float w10 = (vy1 && vx0) ? wy1 * wx0 : 0.f, w11 = (vy1 && vx1) ? wy1 * wx1 : 0.f;
                 const float mask = (w00 + w01 + w10 + w11) > 0.999f ? 1.f : 0.f;
                 float s00[8], s01[8], s10[8], s11[8];
 #pragma unroll
                 for (int j = 0; j < 8; ++j) s00[j] = s01[j] = s10[j] = s11[j] = 0.f;
-                if (w00 != 0.f) load8(sb + ((long long)y0 * w + x0) * a.second.ld + g * 8, s00);
-                if (w01 != 0.f) load8(sb + ((long long)y0 * w + x1) * a.second.ld + g * 8, s01);
-                if (w10 != 0.f) load8(sb + ((long long)y1 * w + x0) * a.second.ld + g * 8, s10);
-                if (w11 != 0.f) load8(sb + ((long long)y1 * w + x1) * a.second.ld + g * 8, s11);
+                if (w00 != 0.f) load8(sb + ((long long)y0 * W + x0) * a.second.ld + g * 8, s00);
+                if (w01 != 0.f) load8(sb + ((long long)y0 * W + x1) * a.second.ld + g * 8, s01);
+                if (w10 != 0.f) load8(sb + ((long long)y1 * W + x0) * a.second.ld + g * 8, s10);
+                if (w11 != 0.f) load8(sb + ((long long)y1 * W + x1) * a.second.ld + g * 8, s11);
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     float vv = 0.f;
@@ -549,53 +554,87 @@ __global__ __launch_bounds__(256) void pwc_level_prep_kernel(PrepArgs a) {
                     v[j] = vv * mask;
                 }
             }
-            store8(wrp + ((y + 4) * bw + x + 4) * Cp + g * 8, v);
+            store8(wrp + ((y + 4) * BW + x + 4) * CP + g * 8, v);
         }
     }
     __syncthreads();
-    // ---- correlation + LeakyReLU into D[c0 + d]; assembly of [first | upflow | upfeat] ----
+    // ---- correlation + LeakyReLU into D[c0 + d] ----
     T* dst = img_ptr<T>(a.D, pair);
-    {
-        const int ns = 256 / npix > 81 ? 81 : (256 / npix > 0 ? 256 / npix : 1);
-        for (int i = t; i < npix * ns; i += 256) {
-            const int q = i % npix, sl = i / npix;
-            const int y = q / w, x = q - (q / w) * w;
-            const T* fa = fst + q * Cp;
+    if constexpr (H >= 8) {
+        // on MFMA: for output row y and displacement row dy, G[x][x'] = sum_c first[y][x][c] second[y+dy][x'][c]
+        // over a 16-wide window of x' (the zero border supplies the out-of-frame columns and rows);
+        // out[y][x][(dy+4)*9 + dx+4] = G[x][x+dx] / C.  H = 16: windows x' in [-4, 12) for x < 8 and [4, 20)
+        // for x >= 8; H = 8: one window [-4, 12), accumulator rows x >= 8 unused.
+        constexpr int NWIN = H == 16 ? 2 : 1, NKS = CP / 32;
+        for (int job = wave; job < H * 9 * NWIN; job += 4) {
+            const int win = job % NWIN, dyi = (job / NWIN) % 9, y = job / (NWIN * 9);
+            const int x0 = win * 8 - 4;                    // first window column
+            const int ya = y + dyi - 4;                    // second-feature row (-4..H+3)
+            f32x4_t acc = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks) {
+                const bf16x8_t A = *(const bf16x8_t*)(fst + (y * W + (col < W ? col : 0)) * CP + ks * 32 + kgl * 8);
+                const bf16x8_t B = *(const bf16x8_t*)(wrp + ((ya + 4) * BW + x0 + col + 4) * CP + ks * 32 + kgl * 8);
+                acc = mfma16<T>(A, B, acc);
+            }
+            // lane (kgl, col): G[x = 4*kgl + r][x' = x0 + col]
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int x = 4 * kgl + r, dx = x0 + col - x;
+                const bool mine = x < W && (NWIN == 1 || (win == 0) == (x < 8));
+                if (mine && dx >= -4 && dx <= 4) {
+                    float v = acc[r] / (float)C;
+                    v = v > 0.f ? v : 0.1f * v;
+                    elem<T>::st(dst + (long long)(y * W + x) * a.D.ld + dyi * 9 + dx + 4, v);
+                }
+            }
+        }
+    } else {
+        constexpr int NS = 256 / NPIX > 81 ? 81 : 256 / NPIX;
+        for (int i = t; i < NPIX * NS; i += 256) {
+            const int q = i % NPIX, sl = i / NPIX;
+            const int y = q / W, x = q % W;
+            const T* fa = fst + q * CP;
             T* o = dst + (long long)q * a.D.ld;
-            for (int d = sl; d < 81; d += ns) {
-                const int dy = d / 9 - 4, dx = d - (d / 9) * 9 - 4;
-                const T* fb = wrp + ((y + 4 + dy) * bw + x + 4 + dx) * Cp;
+            for (int d = sl; d < 81; d += NS) {
+                const int dy = d / 9 - 4, dx = d % 9 - 4;
+                const T* fb = wrp + ((y + 4 + dy) * BW + x + 4 + dx) * CP;
                 float acc = 0.f;
-                for (int c = 0; c < Cp; c += 8) {
+#pragma unroll
+                for (int c = 0; c < CP; c += 8) {
                     float va[8], vb[8];
                     load8(fa + c, va);
                     load8(fb + c, vb);
 #pragma unroll
                     for (int j = 0; j < 8; ++j) acc = fmaf(va[j], vb[j], acc);
                 }
-                float v = acc / (float)a.C;
+                float v = acc / (float)C;
                 v = v > 0.f ? v : 0.1f * v;
                 elem<T>::st(o + d, v);
             }
         }
     }
-    if (a.has_prev) {
-        const int nc = a.C + 4;
-        for (int i = t; i < npix * nc; i += 256) {
-            const int q = i / nc, c = i - q * nc;
-            const float v = c < a.C ? elem<T>::ld(fst + q * Cp + c) : up[q * 4 + (c - a.C)];
+    // ---- assembly of [first | upflow | upfeat] ----
+    if constexpr (PREV) {
+        constexpr int NC = C + 4;
+        for (int i = t; i < NPIX * NC; i += 256) {
+            const int q = i / NC, c = i % NC;
+            const float v = c < C ? elem<T>::ld(fst + q * CP + c) : up[q * 4 + (c - C)];
             elem<T>::st(dst + (long long)q * a.D.ld + 81 + c, v);
         }
     }
 }
 
+// the level shapes with a specialised kernel: (H, C, previous level) of the 64x64 pyramid (levels 6..2)
+#define DBSR_PREP_LEVELS(X) X(1, 196, false) X(2, 128, true) X(4, 96, true) X(8, 64, true) X(16, 32, true)
+
 }  // namespace (level prep)
 
 extern "C" int dbsr_pwc_level_prep_supported(int h, int w, int c) {
-    const int cp = cpad_i(c);
-    const int part = (h * w / 4) * 32 * 4;              // upfeat partials (reuse the first-feature region)
-    const int img = std::max(h * w * cp * 2 + (h + 8) * (w + 8) * cp * 2, part);
-    return h * w * 16 + img <= PREP_LDS_BYTES && h * w <= 256 ? 1 : 0;
+#define DBSR_PREP_OK(HH, CC, PP) if (h == HH && w == HH && c == CC) return 1;
+    DBSR_PREP_LEVELS(DBSR_PREP_OK)
+#undef DBSR_PREP_OK
+    return 0;
 }
 
 extern "C" int dbsr_pwc_level_prep(int P, int h, int w, int c, float scale, dbsr_tensor first, dbsr_tensor second,
@@ -603,8 +642,8 @@ extern "C" int dbsr_pwc_level_prep(int P, int h, int w, int c, float scale, dbsr
                                    const float* w_upflow, const float* b_upflow, const void* w_upfeat,
                                    const float* b_upfeat, void* stream) {
     DBSR_CHECK_ARG(P > 0 && h > 0 && w > 0 && c > 0, "pwc_level_prep: bad sizes");
-    DBSR_CHECK_ARG(dbsr_pwc_level_prep_supported(h, w, c), "pwc_level_prep: %dx%d x %d channels exceed the LDS tile",
-                   h, w, c);
+    DBSR_CHECK_ARG(dbsr_pwc_level_prep_supported(h, w, c), "pwc_level_prep: no kernel for a %dx%d level of %d channels "
+                   "(dbsr_pwc_level_prep_supported)", h, w, c);
     DBSR_CHECK_ARG(first.ptr && second.ptr && D.ptr && first.map.fpg > 0 && second.map.fpg > 0 && D.map.fpg > 0,
                    "pwc_level_prep: null tensor");
     DBSR_CHECK_ARG((first.dtype == DBSR_BF16 || first.dtype == DBSR_F16) && second.dtype == first.dtype &&
@@ -635,10 +674,19 @@ extern "C" int dbsr_pwc_level_prep(int P, int h, int w, int c, float scale, dbsr
     a.pD = prev_D; a.pflow = prev_flow;
     a.wflow = w_upflow; a.bflow = b_upflow; a.wfeat = w_upfeat; a.bfeat = b_upfeat;
     hipStream_t s = (hipStream_t)stream;
-    if (first.dtype == DBSR_BF16)
-        hipLaunchKernelGGL(pwc_level_prep_kernel<bf16_t>, dim3(P), dim3(256), 0, s, a);
-    else
-        hipLaunchKernelGGL(pwc_level_prep_kernel<f16_t>, dim3(P), dim3(256), 0, s, a);
+    bool launched = false;
+#define DBSR_PREP_LAUNCH(HH, CC, PP)                                                                           \
+    if (!launched && h == HH && c == CC) {                                                                     \
+        DBSR_CHECK_ARG(has_prev == PP, "pwc_level_prep: level %dx%d x %d %s a previous level", h, w, c,          \
+                       PP ? "needs" : "takes no");                                                            \
+        if (first.dtype == DBSR_BF16)                                                                          \
+            hipLaunchKernelGGL((pwc_level_prep_kernel<bf16_t, HH, CC, PP>), dim3(P), dim3(256), 0, s, a);      \
+        else                                                                                                   \
+            hipLaunchKernelGGL((pwc_level_prep_kernel<f16_t, HH, CC, PP>), dim3(P), dim3(256), 0, s, a);       \
+        launched = true;                                                                                       \
+    }
+    DBSR_PREP_LEVELS(DBSR_PREP_LAUNCH)
+#undef DBSR_PREP_LAUNCH
     DBSR_LAUNCH_CHECK();
     return 0;
 }

@@ -326,8 +326,9 @@ def test_cfg5_frame_sharded_4_ranks_fp16(cfg4_case):
     assert rep['rms_clamped'] <= RMS_BAR, rep
 
 
+@pytest.mark.parametrize('size', [(96, 80), (48, 48)])      # 48x48: the per-level specialised dense kernels
 @pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
-def test_pwc_fused_dense_levels(synth_sd, dtype):
+def test_pwc_fused_dense_levels(synth_sd, dtype, size):
     """The fused coarse-level DenseNet (dbsr_pwc_dense, levels 6..3) against the per-conv path on the same
     16-bit inputs, and both against the fp32 oracle PWC-Net (pwcnet.py:248-281): the fused path may not
     be further from the oracle than the per-conv one (the two differ only in summation order and in
@@ -337,8 +338,8 @@ def test_pwc_fused_dense_levels(synth_sd, dtype):
     from oracle import dbsr_oracle as orc
     pre = 'encoder.alignment_net.'
     gen = torch.Generator().manual_seed(5)
-    src = torch.rand(6, 3, 96, 80, generator=gen)
-    tgt = (src + 0.05 * torch.randn(6, 3, 96, 80, generator=gen)).clamp(0, 1)
+    src = torch.rand(6, 3, *size, generator=gen)
+    tgt = (src + 0.05 * torch.randn(6, 3, *size, generator=gen)).clamp(0, 1)
     ref = orc.pwcnet(src, tgt, synth_sd)
     flows = {}
     try:
