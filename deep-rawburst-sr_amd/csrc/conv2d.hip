@@ -1117,12 +1117,15 @@ int pick_pipe(const dbsr_conv_desc* d) {
     if (d->gate.ptr) return 0;                                   // gated (backward) convs: tiled/generic kernels
     if (cin_pad(d->cin) * 2 + 64 > ZERO_PAGE_BYTES || d->cout > 512) return 0;
     if ((long long)d->in_h * d->in_w * d->x.ld * 2 >= (1LL << 31)) return 0;   // 32-bit buffer offsets per frame
-    int cfg = 0, tw = 0, wm = 0;
+    int cfg = 0, tw = 0, th = 8, wm = 0;
     if (d->cout > 32 && d->out_w % 48 == 0) { cfg = 1; tw = 48; wm = 64; }
     else if (d->cout <= 32 && d->out_w % 64 == 0) { cfg = 2; tw = 64; wm = 32; }
-    if (!cfg || d->out_h % 8) return 0;
-    const long long nt = (long long)d->n_frames * (d->out_w / tw) * (d->out_h / 8) * ((d->cout + wm - 1) / wm);
-    return (nt >= 256 || g_pipe_enabled == 2) ? cfg : 0;
+    // 16x16 frames (the PWC level-2 DenseNet and the refiner's first conv, pwcnet.py:123-150,188): one whole
+    // frame per tile; a tile per block is enough to beat the LDS-tiled kernel on their 128 - 576 channels
+    else if (d->cout > 32 && d->out_w == 16 && d->out_h == 16) { cfg = 3; tw = 16; th = 16; wm = 64; }
+    if (!cfg || d->out_h % th) return 0;
+    const long long nt = (long long)d->n_frames * (d->out_w / tw) * (d->out_h / th) * ((d->cout + wm - 1) / wm);
+    return (nt >= (cfg == 3 ? 64 : 256) || g_pipe_enabled == 2) ? cfg : 0;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1470,6 +1473,7 @@ int dispatch_ws(int px, const ConvK& k, const dbsr_conv_desc* d, hipStream_t s) 
 template <typename T>
 int dispatch_pipe(int cfg, const ConvK& k, const dbsr_conv_desc* d, hipStream_t s) {
     if (cfg == 1) return launch_pipe<T, 64, 48, 8>(k, d->n_frames, s);
+    if (cfg == 3) return launch_pipe<T, 64, 16, 16>(k, d->n_frames, s);
     return launch_pipe<T, 32, 64, 8>(k, d->n_frames, s);
 }
 

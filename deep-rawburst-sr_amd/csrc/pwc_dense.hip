@@ -329,22 +329,31 @@ __device__ __forceinline__ void dense_conv(DenseCtx<T, NT>& c, f32x4_t* red) {
                 }
             __builtin_amdgcn_sched_barrier(0);
         }
-#pragma unroll
-        for (int j0 = 16; j0 < S::KPW; j0 += 4) {
-            bf16x8_t A[4], B[4][NT];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                A[j] = *(const bf16x8_t*)(w + dense_piece<LEVEL, I>(kid, j0 + j < S::KPW ? j0 + j : j0) * 512);
-#pragma unroll
-                for (int t = 0; t < NT; ++t) B[j][t] = b_at(j0 + j, t);
-            }
+        // the rest streams from global memory one batch of 4 ahead of its MFMAs
+        if constexpr (S::KPW > 16) {
+            bf16x8_t An[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j)
-                if (j0 + j < S::KPW && j0 + j < nj) {
+                An[j] = *(const bf16x8_t*)(w + dense_piece<LEVEL, I>(kid, 16 + j < S::KPW ? 16 + j : 16) * 512);
 #pragma unroll
-                    for (int t = 0; t < NT; ++t) acc[t] = mma16x16x32<T>(A[j], B[j][t], acc[t]);
+            for (int j0 = 16; j0 < S::KPW; j0 += 4) {
+                bf16x8_t A[4], B[4][NT];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    A[j] = An[j];
+                    const int jn = j0 + 4 + j < S::KPW ? j0 + 4 + j : j0;
+                    if (j0 + 4 < S::KPW) An[j] = *(const bf16x8_t*)(w + dense_piece<LEVEL, I>(kid, jn) * 512);
+#pragma unroll
+                    for (int t = 0; t < NT; ++t) B[j][t] = b_at(j0 + j, t);
                 }
-            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (j0 + j < S::KPW && j0 + j < nj) {
+#pragma unroll
+                        for (int t = 0; t < NT; ++t) acc[t] = mma16x16x32<T>(A[j], B[j][t], acc[t]);
+                    }
+                __builtin_amdgcn_sched_barrier(0);
+            }
         }
         if constexpr (S::KSPLIT > 1) {
             if (kid > 0) {

@@ -324,6 +324,16 @@ class PWCPlanner:
                         .to(W.dtype).contiguous()
             self.dec[level] = ent
         self.ref = [W.conv(net.netRefiner.netMain[i]) for i in range(0, 13, 2)]
+        self._W, self._refiner, self._ref_center = W, net.netRefiner, {}
+
+    def ref_center(self, i):
+        """Refiner conv i reduced to its centre tap (a 1x1 conv), packed once."""
+        if i not in self._ref_center:
+            m = self._refiner.netMain[2 * i]
+            self._ref_center[i] = self._W.conv(types.SimpleNamespace(
+                weight=m.weight.detach()[:, :, 1:2, 1:2].contiguous(), bias=m.bias, stride=(1,), padding=(0,),
+                dilation=(1,)))
+        return self._ref_center[i]
 
     def build(self, plan, dtype, device, nF, Hp, Wp, P, first_map, second_map, rgb, flow_out, rgb_map=IDENTITY):
         """Emit: extractor over the nF frames rgb_map(0..nF-1) of `rgb` ([*,Hp,Wp,8]); decoders over P pairs
@@ -442,7 +452,12 @@ class PWCPlanner:
         bufs = [NHWC(P, h, w, cpad(c), dtype, device) for c in chans]
         x, xc0, cin = D2, 0, BASE_OFF + base2
         for i in range(6):
-            plan.conv(f'pwc.refiner{i}', self.ref[i], P, x, xc0, (h, w), bufs[i], 0, L.ACT_LRELU, cin=cin)
+            pc = self.ref[i]
+            if pc.dil >= h and pc.dil >= w and pc.kh == 3:
+                # dilation >= the level size (refiner 4, d 16, on the 16x16 level of a 64x64 frame): every
+                # off-centre tap reads zero padding, so the conv is exactly its centre tap as a 1x1 conv
+                pc = self.ref_center(i)
+            plan.conv(f'pwc.refiner{i}', pc, P, x, xc0, (h, w), bufs[i], 0, L.ACT_LRELU, cin=cin)
             x, xc0, cin = bufs[i], 0, chans[i]
         plan.conv('pwc.refiner6', self.ref[6], P, x, 0, (h, w), None, 0, L.ACT_NONE, y_desc=flow_out.d(0),
                   res=fl2)

@@ -159,11 +159,16 @@ PIPE_EPI = [
 ]
 
 
-@pytest.mark.parametrize('case', PIPE_EPI)
+# the 16x16-frame tile (PWC level 2 / refiner: 117 - 565 input channels, LeakyReLU)
+PIPE16 = [(2, False, 0, 117, 128, 16), (2, False, 0, 565, 128, 16), (2, False, 0, 373, 96, 16),
+          (2, False, 0, 469, 64, 16)]
+
+
+@pytest.mark.parametrize('case', PIPE_EPI + PIPE16)
 def test_pipe_epilogue_variants(ops_mod, case):
     from dbsr_amd import _lib
-    act, use_res, post, cin, cout = case
-    H, W = (8, 96) if cout > 32 else (8, 128)
+    act, use_res, post, cin, cout = case[:5]
+    H, W = (case[5], case[5]) if len(case) > 5 else ((8, 96) if cout > 32 else (8, 128))
     N = 2
     gen = torch.Generator().manual_seed(cin * 13 + cout + act * 7 + post)
     x = torch.randn(N, cin, H, W, generator=gen)
@@ -172,8 +177,10 @@ def test_pipe_epilogue_variants(ops_mod, case):
     res = torch.randn(N, cout, H, W, generator=gen) if use_res else None
     xb, wb = x.to(torch.bfloat16).float(), w.to(torch.bfloat16).float()
     ref = F.conv2d(xb, wb, b, padding=1)
-    if act:
+    if act == 1:
         ref = F.relu(ref)
+    elif act == 2:
+        ref = F.leaky_relu(ref, 0.1)
     if use_res:
         # the kernel adds the residual to the fp32 conv value and rounds once
         ref = ref + res.to(torch.bfloat16).float()
@@ -186,6 +193,8 @@ def test_pipe_epilogue_variants(ops_mod, case):
             outs[algo] = ops_mod.conv2d(x.to(DEV), w.to(DEV), b.to(DEV), padding=1, act=act,
                                         residual=res.to(DEV) if use_res else None, post_act=post,
                                         compute_dtype=torch.bfloat16).float().cpu()
+            if algo == 3:
+                assert ops_mod.conv2d.last_kernel == 2, ops_mod.conv2d.last_kernel
     finally:
         _lib.lib().dbsr_set_conv_algo(2)
     # bf16 output: one rounding of the fp32 result (2^-8 relative)
