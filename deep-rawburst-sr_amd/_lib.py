@@ -112,6 +112,7 @@ def lib():
             'dbsr_chan_sum': ([c_int, c_int, c_int, Tensor, c_void_p, c_int, c_void_p, c_size_t, c_void_p], c_int),
             'dbsr_l1_loss_backward': ([c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, Tensor, c_void_p,
                                        c_void_p, c_size_t, c_void_p], c_int),
+            'dbsr_relu_grad': ([c_int, c_int, c_int, c_int, c_void_p, c_void_p, Tensor, c_void_p], c_int),
             'dbsr_unshuffle_gate': ([c_int, c_int, c_int, c_int, c_int, Tensor, Tensor, Tensor, c_void_p], c_int),
             'dbsr_fuse_backward': ([c_int, c_int, c_int, c_int, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor,
                                     Tensor, c_void_p], c_int),
@@ -153,7 +154,7 @@ EXPORTED = ['dbsr_abi_version', 'dbsr_last_error', 'dbsr_conv_packed_elems', 'db
             'dbsr_fuse_partial', 'dbsr_fuse_combine', 'dbsr_conv_fuse_softmax', 'dbsr_conv_fuse_ok',
             'dbsr_conv_transpose_k4s2', 'dbsr_pack_burst', 'dbsr_flow_finalize', 'dbsr_gauss_blur3',
             'dbsr_merge_prep', 'dbsr_pwc_assemble', 'dbsr_zero', 'dbsr_conv_wgrad_workspace_bytes', 'dbsr_conv_wgrad',
-            'dbsr_chan_sum_workspace_bytes', 'dbsr_chan_sum', 'dbsr_l1_loss_backward', 'dbsr_unshuffle_gate',
+            'dbsr_chan_sum_workspace_bytes', 'dbsr_chan_sum', 'dbsr_l1_loss_backward', 'dbsr_relu_grad', 'dbsr_unshuffle_gate',
             'dbsr_fuse_backward', 'dbsr_merge_prep_backward', 'dbsr_warp_backward', 'dbsr_enc_grad_gate',
             'dbsr_adam_step', 'dbsr_dgrad_weights',
             'dbsr_resize_bilinear', 'dbsr_gauss_reflect', 'dbsr_color_fit', 'dbsr_color_apply', 'dbsr_pwc_dense',

@@ -274,6 +274,22 @@ __global__ __launch_bounds__(256) void l1_loss_bwd_kernel(int B, int C, int H, i
     if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
 }
 
+// The predictor ReLU's backward from an arbitrary upstream gradient (autograd through DBSRNet.forward, any
+// objective): dpre[b][y][x][c] = [pred > 0] * gout[b][c][y][x] (fp32 NCHW in, NHWC out in the compute dtype).
+template <typename T>
+__global__ __launch_bounds__(256) void relu_grad_kernel(int B, int C, int H, int W, const float* __restrict__ pred,
+                                                        const float* __restrict__ gout, dbsr_tensor dpre) {
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long long)B * H * W) return;
+    const int b = (int)(idx / ((long long)H * W));
+    const int rr = (int)(idx - (long long)b * H * W);
+    T* o = img_ptr<T>(dpre, b) + (long long)rr * dpre.ld;
+    for (int c = 0; c < C; ++c) {
+        const long long off = ((long long)b * C + c) * H * W + rr;
+        elem<T>::st(o + c, pred[off] > 0.f ? gout[off] : 0.f);
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 // PixelShuffle(s) backward with the upsampler's ReLU (upsampling.py:51-58): the gradient of the
 // shuffled, ReLU'd output dS [B][sH][sW][C] (and the forward output S itself as the gate) -> the conv's
@@ -580,6 +596,19 @@ extern "C" int dbsr_l1_loss_backward(int B, int C, int H, int W, int boundary_ig
                        1.0f / count);
     DBSR_LAUNCH_CHECK();
     return 0;
+}
+
+extern "C" int dbsr_relu_grad(int B, int C, int H, int W, const float* pred, const float* gout, dbsr_tensor dpre,
+                              void* stream) {
+    DBSR_CHECK_ARG(pred && gout && map_ok(dpre), "relu_grad: null pointer");
+    DBSR_CHECK_ARG(B > 0 && C > 0 && H > 0 && W > 0 && dpre.ld >= dpre.c0 + C, "relu_grad: bad sizes");
+    return by_dtype(dpre.dtype, [&](auto* tag) {
+        using T = std::remove_pointer_t<decltype(tag)>;
+        hipLaunchKernelGGL((relu_grad_kernel<T>), dim3((unsigned)(((long long)B * H * W + 255) / 256)), dim3(256), 0,
+                           (hipStream_t)stream, B, C, H, W, pred, gout, dpre);
+        DBSR_LAUNCH_CHECK();
+        return 0;
+    });
 }
 
 extern "C" int dbsr_unshuffle_gate(int B, int H, int W, int s, int c, dbsr_tensor ds, dbsr_tensor gate, dbsr_tensor du,

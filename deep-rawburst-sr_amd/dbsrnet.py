@@ -90,6 +90,11 @@ class DBSRNet(nn.Module):
                          overwritten by the next forward of the same shape.
       zero_flow          configs[0]'s identity-flow alignment stub (offsets = 0, no PWC-Net); changing it
                          rebuilds the engine.
+    In training mode with autograd enabled (net.train(), no torch.no_grad()) the forward keeps its
+    activations and `pred` carries a grad_fn: loss.backward() on any objective fills the DBSR parameters'
+    .grad (PWC-Net is frozen, encoders.py:56-61) from the HIP backward kernels, and any torch.optim optimizer
+    steps them (compute dtype float32 or bfloat16).  Evaluation (net.eval() or no_grad) runs the inference
+    engine.
     """
     def __init__(self, encoder, merging, decoder):
         super().__init__()
@@ -102,12 +107,14 @@ class DBSRNet(nn.Module):
         self.zero_flow = False          # config 1's identity-flow alignment stub
         self.graph_zero_copy = False
         self._engine = None
+        self._train_engine = None
 
     def set_compute_dtype(self, dtype):
         if dtype not in (torch.float32, torch.bfloat16, torch.float16):
             raise ValueError('compute_dtype must be torch.float32, torch.bfloat16 or torch.float16')
         self.compute_dtype = dtype
         self._engine = None
+        self._train_engine = None
         return self
 
     def _get_engine(self):
@@ -116,9 +123,20 @@ class DBSRNet(nn.Module):
             self._engine = DBSREngine(self)
         return self._engine
 
+    def _trains(self):
+        """Training mode with autograd on: some DBSR (non-PWC) parameter requires grad."""
+        if not (self.training and torch.is_grad_enabled()):
+            return False
+        return any(p.requires_grad for n, p in self.named_parameters() if not n.startswith('encoder.alignment_net'))
+
     def forward(self, im):
         if im.dim() != 5:
             raise ValueError('expected burst [B,N,4,H,W], got shape {}'.format(tuple(im.shape)))
+        if self._trains():
+            # autograd through the HIP training forward / backward (training.train_forward): the reference's
+            # loop -- pred, _ = net(burst); loss.backward(); optimizer.step() -- runs unchanged
+            from .training import train_forward
+            return train_forward(self, im)
         return self._get_engine().forward(im)
 
 

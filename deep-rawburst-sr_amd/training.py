@@ -97,7 +97,7 @@ class DBSRTrainer:
     encoder: the order the backward completes them, so the bucketed all-reduce can start early).
     """
     def __init__(self, net, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, boundary_ignore=40, process_group=None,
-                 bucket_bytes=4 << 20):
+                 bucket_bytes=4 << 20, optimizer=True):
         dev = next(net.parameters()).device
         if dev.type != 'cuda':
             raise RuntimeError('DBSRTrainer needs the network on a HIP device')
@@ -120,8 +120,9 @@ class DBSRTrainer:
         n = sum(p.numel() for p in self.params)
         self.flat = torch.empty(n, dtype=torch.float32, device=dev)
         self.flat_grad = torch.zeros(n, dtype=torch.float32, device=dev)
-        self.exp_avg = torch.zeros(n, dtype=torch.float32, device=dev)
-        self.exp_avg_sq = torch.zeros(n, dtype=torch.float32, device=dev)
+        # Adam moments (not allocated when an external optimizer steps the parameters: the autograd path)
+        self.exp_avg = torch.zeros(n if optimizer else 0, dtype=torch.float32, device=dev)
+        self.exp_avg_sq = torch.zeros(n if optimizer else 0, dtype=torch.float32, device=dev)
         self.offset = {}
         o = 0
         for p in self.params:
@@ -313,8 +314,13 @@ class DBSRTrainer:
 
         dP = NHWC(B, HS, WS, 8, dt, dev)
         nlb = (B * HS * WS + 255) // 256
+        plan.fwd_end = len(plan.ops)            # ops[:fwd_end]: the forward with saved activations (+ grad zeroing)
         plan.add('l1_loss_bwd', lib.dbsr_l1_loss_backward, B, 3, HS, WS, self.bi, pred.data_ptr(),
                  bufs['gt'].data_ptr(), dP.d(0), self.loss.data_ptr(), ws('l1', 4 * nlb), 4 * nlb)
+        # autograd: the same backward from an upstream dL/dpred instead of the built-in L1 objective
+        bufs['gpred'] = torch.zeros(B, 3, HS, WS, dtype=torch.float32, device=dev)
+        plan.grad_in_op = (lib.dbsr_relu_grad, (B, 3, HS, WS, pred.data_ptr(), bufs['gpred'].data_ptr(), dP.d(0)),
+                           'relu_grad', 0)
         wgrad('dec.predictor', self.pred, B, HS, WS, h_last, 0, dP, 0)
         bgrad('dec.predictor', self.pred, B, HS * WS, dP, 0)
 
@@ -426,6 +432,7 @@ class DBSRTrainer:
                           post_s, scratch])
         plan.bufs = bufs
         plan.buckets = buckets
+        plan.FW, plan.gen = FW, 0
         return plan
 
     # ------------------------------------------------------------------------------------------------
@@ -472,6 +479,42 @@ class DBSRTrainer:
         plan.bufs['gt'].copy_(frame_gt.to(torch.float32), non_blocking=True)
         plan.run(L.stream_ptr(self.dev))
         return self.loss, plan.bufs['pred']
+
+    # ---- autograd through DBSRNet.forward (the reference's own loop: pred, _ = net(burst); objective(pred,
+    # gt).backward(); optimizer.step(); actors/dbsr_actors.py:27-47, trainers/simple_trainer.py:78-81) ----
+    def _plan(self, shape):
+        B, N, _, H, W = shape
+        key = (B, N, H, W)
+        plan = self.plans.get(key)
+        if plan is None:
+            plan = self.plans[key] = self._build(B, N, H, W)
+        return plan
+
+    def forward_saved(self, burst):
+        """The training forward with every activation kept in the plan's buffers: (pred, offsets, fusion
+        weights, token).  The activations stay valid until the next forward of the same shape; `token`
+        names them for backward_from."""
+        plan = self._plan(burst.shape)
+        plan.bufs['burst'].copy_(burst.to(torch.float32), non_blocking=True)
+        plan.run_list(plan.ops[:plan.fwd_end], L.stream_ptr(self.dev))
+        plan.gen += 1
+        B, N, _, H, W = burst.shape
+        fw = plan.FW.t.view(B, N, H, W, -1).permute(0, 1, 4, 2, 3)
+        return plan.bufs['pred'].clone(), plan.bufs['offsets'].view(B, N - 1, 2, H, W).clone(), fw.clone(), \
+            (plan, plan.gen)
+
+    def backward_from(self, token, gpred):
+        """Gradients of the DBSR parameters (list in self.params order, fp32) from dL/dpred of the forward
+        that returned `token`."""
+        plan, gen = token
+        if plan.gen != gen:
+            raise RuntimeError('DBSRNet training: backward() after another forward of the same burst shape -- the '
+                               'saved activations are gone (one forward per backward, as in the reference loop)')
+        plan.bufs['gpred'].copy_(gpred.to(torch.float32), non_blocking=True)
+        fn, args, name, _ = plan.grad_in_op
+        L.check(fn(*args, L.stream_ptr(self.dev)), name)
+        plan.run_list(plan.ops[plan.fwd_end + 1:], L.stream_ptr(self.dev))
+        return [self.flat_grad[o:o + k].view(p.shape).clone() for p in self.params for (o, k) in [self.offset[id(p)]]]
 
     def grads(self):
         """{parameter name: gradient} views of the flat gradient buffer."""
@@ -528,3 +571,30 @@ def allreduce_bucket(flat_grad, lo, hi, group=None):
     """Start the sum all-reduce of one gradient bucket (RCCL on HIP tensors, gloo on CPU tensors); the
     caller scales by 1/world (folded into the Adam step)."""
     return dist.all_reduce(flat_grad[lo:hi], group=group, async_op=True)
+
+
+class _DBSRTrainForward(torch.autograd.Function):
+    """DBSRNet.forward under autograd: the HIP training forward (activations saved) and, on backward, the
+    HIP backward from dL/dpred into the DBSR parameters' gradients (PWC-Net is frozen, encoders.py:56-61)."""
+
+    @staticmethod
+    def forward(ctx, burst, engine, *params):
+        pred, offs, fw, token = engine.forward_saved(burst)
+        ctx.engine, ctx.token = engine, token
+        ctx.mark_non_differentiable(offs, fw)
+        return pred, offs, fw
+
+    @staticmethod
+    def backward(ctx, gpred, goffs, gfw):
+        if gpred is None:
+            return (None, None) + tuple(None for _ in ctx.engine.params)
+        return (None, None) + tuple(ctx.engine.backward_from(ctx.token, gpred.contiguous()))
+
+
+def train_forward(net, burst):
+    """pred, {'offsets', 'fusion_weights'} of DBSRNet.forward with autograd to the DBSR parameters."""
+    eng = getattr(net, '_train_engine', None)
+    if eng is None or eng.net is not net or eng.dtype != net.compute_dtype:
+        eng = net._train_engine = DBSRTrainer(net, optimizer=False)
+    pred, offs, fw = _DBSRTrainForward.apply(burst, eng, *eng.params)
+    return pred, {'offsets': offs, 'fusion_weights': fw}

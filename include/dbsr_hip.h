@@ -291,6 +291,9 @@ int dbsr_chan_sum(int n, int hw, int c, dbsr_tensor t, float* out, int accumulat
  * sign(pred - gt) / count inside the crop, 0 outside.  workspace: >= ceil(B*H*W/256) floats. */
 int dbsr_l1_loss_backward(int B, int C, int H, int W, int boundary_ignore, const float* pred, const float* gt,
                           dbsr_tensor dpre, float* loss, void* workspace, size_t workspace_bytes, void* stream);
+/* The RGB predictor's ReLU backward from an upstream gradient (autograd through DBSRNet.forward with any
+ * objective): dpre (NHWC, C channels, compute dtype) = [pred > 0] * gout; pred / gout fp32 NCHW [B][C][H][W]. */
+int dbsr_relu_grad(int B, int C, int H, int W, const float* pred, const float* gout, dbsr_tensor dpre, void* stream);
 /* PixelShuffle(s) + ReLU backward (upsampling.py:51-58): du[b][y][x][c*s*s + i*s + j] =
  * ds[b][y*s+i][x*s+j][c] * [gate > 0] (gate = the upsampler's forward output). */
 int dbsr_unshuffle_gate(int B, int H, int W, int s, int c, dbsr_tensor ds, dbsr_tensor gate, dbsr_tensor du,

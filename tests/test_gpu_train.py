@@ -180,3 +180,90 @@ def test_cfg4_training_steps_bf16(synth_sd):
     print('losses', losses)
     assert all(np.isfinite(losses))
     assert losses[-1] < losses[0]
+
+
+# ----------------------------------------------------------------------------------------------------
+# autograd through DBSRNet.forward: the reference's own loop, unchanged
+# ----------------------------------------------------------------------------------------------------
+def _objective(name, pred, gt, bi=40):
+    p, g = pred[..., bi:-bi, bi:-bi], gt[..., bi:-bi, bi:-bi]
+    return F.l1_loss(p, g) if name == 'l1' else F.mse_loss(p, g)
+
+
+@pytest.mark.parametrize('dtype,objective', [(torch.float32, 'l1'), (torch.float32, 'mse'), (torch.bfloat16, 'l1')])
+def test_autograd_reference_loop(synth_sd, dtype, objective):
+    """actors/dbsr_actors.py:27-47 + trainers/simple_trainer.py:78-81 as written: pred, _ = net(burst);
+    loss = objective(pred, gt); optimizer.zero_grad(); loss.backward(); optimizer.step() -- with
+    torch.optim.Adam over the DBSR parameters.  The .grad the HIP backward leaves behind matches autograd
+    through the oracle (the tolerances of test_train_step_grads_vs_oracle), the step moves the weights, a
+    second iteration runs, and eval mode then serves the updated weights through the inference engine."""
+    import dbsr_amd
+    from dbsr_amd.burst import synthetic_bursts
+    from oracle import dbsr_oracle as orc
+    burst, gt = synthetic_bursts(2, 3, 24, 32, sr_factor=8, seed=17)
+    sd = {k: v.clone().requires_grad_(not k.startswith('encoder.alignment_net')) for k, v in synth_sd.items()}
+    rpred, _ = orc.dbsr_forward(burst, sd)
+    rloss = _objective(objective, rpred, gt)
+    rloss.backward()
+    ref_g = {k: v.grad for k, v in sd.items() if v.grad is not None}
+    net = dbsr_amd.dbsrnet_cvpr2021(**dbsr_amd.DBSR_SYNTHETIC_KWARGS)
+    net.load_state_dict(synth_sd)
+    net = net.to(DEV).set_compute_dtype(dtype).train()
+    for p in net.encoder.alignment_net.parameters():
+        p.requires_grad_(False)                          # train_alignmentnet=False (encoders.py:56-61)
+    params = [p for p in net.parameters() if p.requires_grad]
+    opt = torch.optim.Adam(params, lr=1e-4)
+    b, g = burst.to(DEV), gt.to(DEV)
+    pred, aux = net(b)
+    assert pred.grad_fn is not None and aux['offsets'].shape == (2, 2, 2, 24, 32)
+    loss = _objective(objective, pred, g)
+    opt.zero_grad()
+    loss.backward()
+    mine = {k: p.grad.cpu() for k, p in net.named_parameters() if p.grad is not None}
+    assert set(mine) == set(ref_g), set(mine) ^ set(ref_g)
+    gmax = max(float(x.abs().max()) for x in ref_g.values())
+    rel, cos = [], []
+    for k, gr in ref_g.items():
+        if k == 'merging.weight_predictor.4.0.bias':     # exact gradient 0 (softmax shift invariance)
+            assert float(mine[k].abs().max()) <= 1e-4 * gmax
+            continue
+        rel.append((_rel(mine[k], gr), k))
+        cos.append((1 - float(F.cosine_similarity(mine[k].double().flatten(), gr.double().flatten(), dim=0)), k))
+    rel.sort(reverse=True)
+    cos.sort(reverse=True)
+    print(objective, dtype, 'loss', float(loss), float(rloss), 'max-rel worst', rel[:2], '1-cos worst', cos[:2])
+    if dtype == torch.float32:
+        assert abs(float(loss) - float(rloss)) <= 1e-5 * max(1.0, abs(float(rloss)))
+        assert rel[0][0] <= 2e-2 and cos[0][0] <= 1e-4, (rel[:3], cos[:3])
+    else:
+        assert abs(float(loss) - float(rloss)) <= 1e-2 * abs(float(rloss))
+        assert cos[0][0] <= 3e-2, cos[:3]
+    before = [p.detach().clone() for p in params]
+    opt.step()
+    assert all(not torch.equal(a, p.detach()) for a, p in zip(before, params))
+    pred2, _ = net(b)                                    # second iteration on the updated weights
+    loss2 = _objective(objective, pred2, g)
+    opt.zero_grad()
+    loss2.backward()
+    opt.step()
+    assert torch.isfinite(loss2) and all(torch.isfinite(p.grad).all() for p in params)
+    net.eval()
+    with torch.no_grad():
+        pe, _ = net(b)                                   # inference engine, repacked from the updated weights
+    pt, _ = net.train()(b)
+    assert float((pe.float() - pt.detach().float()).abs().max()) <= (1e-3 if dtype == torch.float32 else 0.1)
+
+
+def test_autograd_backward_after_second_forward_raises(synth_sd):
+    import dbsr_amd
+    from dbsr_amd.burst import synthetic_bursts
+    burst, _ = synthetic_bursts(1, 3, 24, 32, sr_factor=8, seed=3)
+    net = dbsr_amd.dbsrnet_cvpr2021(**dbsr_amd.DBSR_SYNTHETIC_KWARGS)
+    net.load_state_dict(synth_sd)
+    net = net.to(DEV).train()
+    b = burst.to(DEV)
+    p1, _ = net(b)
+    p2, _ = net(b)
+    p2.sum().backward()
+    with pytest.raises(RuntimeError, match='saved activations'):
+        p1.sum().backward()

@@ -214,3 +214,20 @@ def test_bench_rejects_gpus_world_mismatch():
     out = subprocess.run([sys.executable, os.path.join(repo, 'bench.py'), '--gpus', '2', '--dry-run'],
                          capture_output=True, text=True, timeout=120, env=env, cwd=repo)
     assert out.returncode != 0 and 'one rank per GPU' in out.stderr
+
+
+def test_dbsrnet_training_mode_dispatch():
+    """net.train() with autograd routes DBSRNet.forward to the HIP training path (saved activations + HIP
+    backward); eval / no_grad / frozen DBSR parameters route it to the inference engine (CPU check of the
+    dispatch only)."""
+    import dbsr_amd
+    net = dbsr_amd.dbsrnet_cvpr2021(**dbsr_amd.DBSR_SYNTHETIC_KWARGS)
+    assert net.train()._trains()
+    with torch.no_grad():
+        assert not net._trains()
+    assert not net.eval()._trains()
+    net.train()
+    for n, p in net.named_parameters():
+        if not n.startswith('encoder.alignment_net'):
+            p.requires_grad_(False)
+    assert not net._trains()
