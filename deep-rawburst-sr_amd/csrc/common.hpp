@@ -12,13 +12,16 @@ typedef __attribute__((ext_vector_type(8))) short bf16x8_t;        // MFMA 16-bi
 typedef __attribute__((ext_vector_type(4))) float f32x4_t;          // 16x16 MFMA accumulator
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
 
-// The LDS-DMA-staged MFMA conv kernels (pipelined and two-barrier tiled) claim the whole VGPR file of
-// their SIMDs (v255 marked live -> 256 VGPRs per wave; their 2 waves per SIMD then fill its 512), so no
-// wave of another kernel is ever co-resident with them.  Measured ('two-lane race'): with
-// another stream's kernels sharing their CUs, waves of those kernels computed wrong values from correct
-// inputs (an instrumented PWC backwarp wave read the right flow and produced a wrong bilinear mass);
-// no stray write, kernarg, stream-order or workspace-aliasing cause reproduced it, and exclusive SIMDs
-// remove it.  Costs nothing at 2 waves per SIMD (their occupancy is already 2).
+// The LDS-DMA-staged MFMA conv kernels (pipelined, weight-stationary, two-barrier tiled) claim the whole VGPR
+// file of their SIMDs (v255 marked live -> 256 VGPRs per wave; their 2 waves per SIMD then fill its 512), so no
+// wave of another kernel is ever co-resident with them.  This is a WORKAROUND FOR AN UNEXPLAINED RACE, not a
+// fix ('The two-lane race'): with another stream's kernels sharing their CUs, waves of those kernels
+// computed wrong values from correct inputs (an instrumented PWC backwarp wave read the right flow and
+// produced a wrong bilinear mass); exclusive SIMDs remove it.  Ruled out so far: stray writes, kernargs,
+// stream order, split-K workspace aliasing, and -- by the static ISA audit of the shipped code objects
+// (tools/isa_audit.py, tests/test_capi.py) -- under-declared VGPR/AGPR counts, LDS-DMA without M0 set in the
+// same basic block, and LDS use beyond the declared group segment.  The audit also fails any future LDS-DMA
+// kernel that does not claim its SIMDs.  Costs nothing at 2 waves per SIMD (their occupancy is already 2).
 #define DBSR_OWN_SIMDS() asm volatile("" ::: "v255")
 
 __device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((unsigned)v) << 16); }

@@ -152,3 +152,18 @@ def test_torch_ops_registered():
     # HIP implementations only (no CPU kernel, like correlation.py:324-325): CPU tensors fail loudly
     with pytest.raises(NotImplementedError, match="dbsr::correlation.*CPU"):
         torch.ops.dbsr.correlation(torch.zeros(1, 4, 3, 3), torch.zeros(1, 4, 3, 3))
+
+
+def test_lds_dma_kernels_own_their_simds():
+    """Static ISA audit of the shipped code objects (tools/isa_audit.py): every
+    kernel issuing LDS-DMA declares the registers its code uses, sets M0 in the same basic block before each
+    LDS-DMA instruction, fits its declared LDS, and (DBSR_OWN_SIMDS) claims the whole register file of its
+    SIMDs, so a future LDS-DMA kernel without the marker fails here instead of silently racing."""
+    import importlib.util
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location('isa_audit', os.path.join(repo, 'tools', 'isa_audit.py'))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    rows, bad = mod.audit(os.path.join(repo, 'deep-rawburst-sr_amd', 'libdbsr_hip.so'))
+    assert len(rows) >= 40, 'expected the pipelined / weight-stationary / tiled LDS-DMA kernels'
+    assert not bad, bad
