@@ -79,6 +79,17 @@ class NHWC:
     def d(self, c0=0, fmap=IDENTITY):
         return L.tensor_desc(self.t, self.ld, c0, img_stride=self.h * self.w * self.ld, fmap=fmap)
 
+    def rows(self, y0, y1):
+        """Rows [y0, y1) of every image as an image of y1 - y0 rows (a view: convs treat the rows outside it
+        as zero padding)."""
+        v = NHWC.__new__(NHWC)
+        v.n, v.h, v.w, v.ld, v.dtype = self.n, y1 - y0, self.w, self.ld, self.dtype
+        v.t = self.t[:, y0:y1]
+        v.full_h = self.h
+        v.d = lambda c0=0, fmap=IDENTITY: L.tensor_desc(v.t, v.ld, c0, img_stride=self.h * self.w * self.ld,
+                                                        fmap=fmap)
+        return v
+
 
 class PackedConv:
     """One nn.Conv2d packed for dbsr_conv2d."""
@@ -906,8 +917,16 @@ class DBSREngine:
         return pred.view(pred.shape), aux
 
     # ---------------- frame-sharded fusion (BASELINE configs[4]) ----------------
-    def _build_combine(self, R, B, H, W):
-        """dbsr_fuse_combine of R ranks' gathered statistics -> FUS, then the decoder."""
+    def decoder_halo(self):
+        """LR rows of context the decoder needs beyond a row slab for the slab's prediction to be exact: one per
+        LR 3x3 conv (init + pre ResBlocks) plus the HR 3x3 convs (blur + post ResBlocks) in LR rows."""
+        from .parallel import decoder_halo_rows
+        return decoder_halo_rows(len(self.dec_pre), len(self.dec_post), self.s, self.blur is not None)
+
+    def _build_combine(self, R, B, H, W, rows=None):
+        """dbsr_fuse_combine of R ranks' gathered statistics -> FUS, then the decoder -- over all rows, or (frame
+        sharding with a split decoder) over LR rows `rows` = [lo, hi) widened by decoder_halo() rows on each side
+        (the prediction of [lo, hi) is then exactly the unsplit one)."""
         dt, dev = self.dtype, self.device
         C = self.enc_out.cout
         plan = Plan()
@@ -915,7 +934,22 @@ class DBSREngine:
         FUS = NHWC(B, H, W, C, dt, dev)
         plan.add('merge.fuse_combine', L.lib().dbsr_fuse_combine, R, B, H * W, C, bufs['gathered'].data_ptr(),
                  FUS.d(0))
-        self._decoder(plan, B, H, W, FUS, bufs)
+        if rows is None:
+            self._decoder(plan, B, H, W, FUS, bufs)
+            plan.valid = (0, H * self.s)
+        else:
+            lo, hi = rows
+            halo = self.decoder_halo()
+            y0, y1 = max(0, lo - halo), min(H, hi + halo)
+            # widen the slab to a multiple of 16 rows where the image allows (the trunk kernels' tile height;
+            # extra context leaves the valid rows exact)
+            while (y1 - y0) % 16 and (y0 > 0 or y1 < H):
+                if y0 > 0:
+                    y0 -= 1
+                else:
+                    y1 += 1
+            self._decoder(plan, B, y1 - y0, W, FUS.rows(y0, y1), bufs)
+            plan.valid = ((lo - y0) * self.s, (hi - y0) * self.s)
         plan.keep.append(FUS)
         plan.finalize_workspace(dev)
         plan.bufs = bufs
@@ -944,26 +978,30 @@ class DBSREngine:
         plan.run(L.stream_ptr(burst.device))
         return plan.bufs['stats'], plan.bufs['offsets'].view(B, N - 1, 2, H, W)
 
-    def gathered_buffer(self, R, B, H, W):
+    def gathered_buffer(self, R, B, H, W, rows=None):
         """The combine plan's input buffer [R,B,H,W,3C] fp32: all-gather the ranks' stats straight into it."""
         if self.device is None:
             raise RuntimeError('gathered_buffer: run forward_partial first (the engine packs its weights there)')
-        key = ('combine', R, B, H, W)
+        key = ('combine', R, B, H, W, rows)
         plan = self.plans.get(key)
         if plan is None:
-            plan = self.plans[key] = self._build_combine(R, B, H, W)
+            plan = self.plans[key] = self._build_combine(R, B, H, W, rows)
         return plan.bufs['gathered']
 
-    def combine_decode(self, gathered):
-        """Log-sum-exp combine of gathered [R,B,H,W,3C] statistics + decoder -> pred [B,3,sH,sW] (clone)."""
+    def combine_decode(self, gathered, rows=None):
+        """Log-sum-exp combine of gathered [R,B,H,W,3C] statistics + decoder -> pred [B,3,sH,sW] (clone); with
+        rows = [lo, hi) (LR rows) only the prediction rows [s*lo, s*hi), from a decoder run on that slab plus
+        its halo."""
         self._ready(gathered)
         R, B, H, W = gathered.shape[:4]
-        buf = self.gathered_buffer(R, B, H, W)
+        rows = None if rows is None else (int(rows[0]), int(rows[1]))
+        buf = self.gathered_buffer(R, B, H, W, rows)
         if buf.data_ptr() != gathered.data_ptr():
             buf.copy_(gathered, non_blocking=True)
-        plan = self.plans[('combine', R, B, H, W)]
+        plan = self.plans[('combine', R, B, H, W, rows)]
         plan.run(L.stream_ptr(gathered.device))
-        return plan.bufs['pred'].clone()
+        a, b = plan.valid
+        return plan.bufs['pred'][:, :, a:b].clone()
 
 
 # ==================================================================================================

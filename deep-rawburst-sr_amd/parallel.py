@@ -64,7 +64,9 @@ def run_sharded(net, bursts):
 # the burst (merging.py:116-124): each rank reduces its own frames to (max, sum exp, sum exp*feat)
 # statistics, one all-gather moves them (3*C*H*W fp32 per burst per rank -- instead of gathering the
 # warped 512-channel features of every frame), and a log-sum-exp combine rebuilds the fused embedding.
-# The decoder then runs on every rank (redundant, it is per burst).
+# The decoder is split by rows: rank r decodes LR rows shard_range(H, r, R) plus the decoder's receptive-field
+# halo (DBSREngine.decoder_halo: one LR row per LR 3x3 conv, the HR 3x3 convs in LR rows), which makes its rows of
+# the prediction exactly the unsplit ones; one all-gather assembles the prediction.
 # ---------------------------------------------------------------------------------------------------
 def frame_shard(num_frames, rank, world):
     """Frame indices rank `rank` processes: [0] + its contiguous share of frames 1..N-1, and the first
@@ -76,11 +78,34 @@ def frame_shard(num_frames, rank, world):
     return [0] + list(range(1 + a, 1 + b)), (0 if rank == 0 else 1)
 
 
-def frame_sharded_forward(net, burst, partial_fn=None, combine_fn=None, gathered_fn=None):
+def decoder_halo_rows(n_pre, n_post, s, blur=True):
+    """LR rows of context a row slab of the decoder (decoders.py:54-62) needs for an exact prediction: one per
+    LR 3x3 conv (init + 2 per pre-ResBlock), plus the HR 3x3 convs (blur + 2 per post-ResBlock) in LR rows."""
+    n_lr = 1 + 2 * n_pre
+    n_hr = 2 * n_post + (1 if blur else 0)
+    return n_lr + (n_hr + s - 1) // s
+
+
+def gather_rows(slab, total_rows, rows_per_lr=1):
+    """All-gather per-rank row slabs [B, C, r_i, W] (rank r holds LR rows shard_range(total_rows, r, R), i.e.
+    rows_per_lr times as many prediction rows) into [B, C, rows_per_lr * total_rows, W] in rank order."""
+    world = dist.get_world_size()
+    sizes = [(b - a) * rows_per_lr for a, b in (shard_range(total_rows, r, world) for r in range(world))]
+    mx = max(sizes)
+    pad = slab.new_zeros(slab.shape[:2] + (mx,) + slab.shape[3:])
+    pad[:, :, :slab.shape[2]] = slab
+    bufs = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(bufs, pad.contiguous())
+    return torch.cat([bf[:, :, :n] for bf, n in zip(bufs, sizes)], dim=2)
+
+
+def frame_sharded_forward(net, burst, partial_fn=None, combine_fn=None, gathered_fn=None, split_decoder=True):
     """pred [B,3,sH,sW] of `burst` [B,N,4,H,W] (same on every rank) with its frames sharded over the
-    process group.  partial_fn(local_burst, first) -> stats and combine_fn(gathered [R,...]) -> pred
-    default to the HIP engine (DBSREngine.forward_partial / combine_decode); gathered_fn(R, stats) gives
-    the all-gather destination (the engine's combine input buffer, so the collective writes in place)."""
+    process group.  partial_fn(local_burst, first) -> stats and combine_fn(gathered [R,...], rows) -> pred rows
+    default to the HIP engine (DBSREngine.forward_partial / combine_decode); gathered_fn(R, stats, rows) gives
+    the all-gather destination (the engine's combine input buffer, so the collective writes in place).
+    split_decoder: each rank decodes its LR rows shard_range(H, rank, R) (+ halo) and one all-gather assembles
+    the prediction; False: every rank decodes the whole image."""
     rank, world = dist.get_rank(), dist.get_world_size()
     frames, first = frame_shard(burst.shape[1], rank, world)
     local = burst[:, frames]
@@ -88,10 +113,15 @@ def frame_sharded_forward(net, burst, partial_fn=None, combine_fn=None, gathered
         eng = net._get_engine()
         partial_fn = lambda x, f: eng.forward_partial(x, f)[0]                          # noqa: E731
         combine_fn = eng.combine_decode
-        gathered_fn = lambda R, st: eng.gathered_buffer(R, *st.shape[:3])              # noqa: E731
+        gathered_fn = lambda R, st, rows: eng.gathered_buffer(R, *st.shape[:3], rows)  # noqa: E731
+    H = burst.shape[-2]
+    rows = shard_range(H, rank, world) if split_decoder else None
     stats = partial_fn(local, first)
-    gathered = gathered_fn(world, stats) if gathered_fn is not None else \
+    gathered = gathered_fn(world, stats, rows) if gathered_fn is not None else \
         stats.new_empty((world,) + tuple(stats.shape))
     # concatenated along dim 0 ([R*B,...] view of the [R,B,...] buffer): the layout gloo and RCCL both take
     dist.all_gather_into_tensor(gathered.view((-1,) + tuple(stats.shape[1:])), stats.contiguous())
-    return combine_fn(gathered)
+    if not split_decoder:
+        return combine_fn(gathered)
+    slab = combine_fn(gathered, rows)
+    return gather_rows(slab, H, slab.shape[3] // burst.shape[-1])
