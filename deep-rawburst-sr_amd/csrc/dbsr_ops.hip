@@ -798,6 +798,42 @@ extern "C" int dbsr_fuse_combine(int R, int B, int hw, int c, const float* stats
     });
 }
 
+namespace {
+// NHWC (16-bit or fp32) -> fp32 NCHW, per image: out[img][c][p] = in[img][p][c].  64 pixels x 64 channels per
+// block through a padded LDS tile: both the reads (channels of a pixel) and the writes (pixels of a channel)
+// are coalesced.  The aux fusion weights in the reference's layout (merging.py:117-126 returns the fp32
+// softmax [B,N,C,H,W]), materialised only when a caller reads them.
+template <typename T>
+__global__ __launch_bounds__(256) void nhwc_to_nchw_kernel(int hw, int C, dbsr_tensor in, float* __restrict__ out) {
+    __shared__ float tile[64][65];
+    const int img = blockIdx.z, p0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
+    const T* src = img_ptr<T>(in, img);
+    for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+        const int pl = i / 64, cl = i % 64;
+        const int p = p0 + pl, c = c0 + cl;
+        tile[pl][cl] = (p < hw && c < C) ? elem<T>::ld(src + (long long)p * in.ld + c) : 0.f;
+    }
+    __syncthreads();
+    float* dst = out + (long long)img * C * hw;
+    for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+        const int cl = i / 64, pl = i % 64;
+        const int p = p0 + pl, c = c0 + cl;
+        if (p < hw && c < C) dst[(long long)c * hw + p] = tile[pl][cl];
+    }
+}
+}  // namespace
+
+extern "C" int dbsr_nhwc_to_nchw_f32(int n, int hw, int c, dbsr_tensor in, float* out, void* stream) {
+    DBSR_CHECK_ARG(map_ok(in) && out && n > 0 && hw > 0 && c > 0 && in.c0 + c <= in.ld, "nhwc_to_nchw: bad tensor");
+    return by_dtype(in.dtype, [&](auto* tag) {
+        using T = std::remove_pointer_t<decltype(tag)>;
+        hipLaunchKernelGGL(nhwc_to_nchw_kernel<T>, dim3((unsigned)((hw + 63) / 64), (unsigned)((c + 63) / 64), (unsigned)n),
+                           dim3(256), 0, (hipStream_t)stream, hw, c, in, out);
+        DBSR_LAUNCH_CHECK();
+        return 0;
+    });
+}
+
 extern "C" int dbsr_merge_prep(int B, int N, int hw, int c, dbsr_tensor proj, dbsr_tensor out, void* stream) {
     DBSR_CHECK_ARG(map_ok(proj) && map_ok(out) && proj.dtype == out.dtype, "merge_prep: bad tensor");
     DBSR_CHECK_ARG(c % 8 == 0 && vec_ok(proj, 8) && vec_ok(out, 8) && out.c0 + 2 * c <= out.ld, "merge_prep: layout");

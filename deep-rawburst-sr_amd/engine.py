@@ -91,6 +91,54 @@ class NHWC:
         return v
 
 
+class DBSRAux(dict):
+    """aux of DBSRNet.forward, {'offsets', 'fusion_weights'} as dbsrnet.py:38 returns it.  'fusion_weights' is
+    the reference's tensor -- fp32, contiguous [B,N,C,H,W] (merging.py:117-126) -- materialised from the
+    engine's channels-last buffer by dbsr_nhwc_to_nchw_f32 the first time it is read (the reference's callers
+    never read it, so a forward does not pay for the transpose); `native_fusion_weights` is the zero-copy
+    [B,N,C,H,W] view of the channels-last buffer in the compute dtype."""
+
+    def __init__(self, offsets, native_fw):
+        super().__init__(offsets=offsets, fusion_weights=None)
+        self.native_fusion_weights = native_fw          # [B,N,C,H,W] view of [B*N,H,W,C] storage, or None
+        self._done = native_fw is None
+
+    def _materialize(self):
+        if self._done:
+            return
+        v = self.native_fusion_weights
+        B, N, C, H, W = v.shape
+        src = v.permute(0, 1, 3, 4, 2)                  # back to the storage order [B,N,H,W,C]
+        out = torch.empty(B, N, C, H, W, dtype=torch.float32, device=v.device)
+        L.check(L.lib().dbsr_nhwc_to_nchw_f32(B * N, H * W, C, L.tensor_desc(src, src.stride(-2), 0,
+                                                                               img_stride=src.stride(1)),
+                                              out.data_ptr(), L.stream_ptr(v.device)), 'dbsr_nhwc_to_nchw_f32')
+        dict.__setitem__(self, 'fusion_weights', out)
+        self._done = True
+
+    def __getitem__(self, k):
+        if k == 'fusion_weights':
+            self._materialize()
+        return dict.__getitem__(self, k)
+
+    def get(self, k, default=None):
+        if k == 'fusion_weights':
+            self._materialize()
+        return dict.get(self, k, default)
+
+    def items(self):
+        self._materialize()
+        return dict.items(self)
+
+    def values(self):
+        self._materialize()
+        return dict.values(self)
+
+    def copy(self):
+        self._materialize()
+        return dict(self)
+
+
 class PackedConv:
     """One nn.Conv2d packed for dbsr_conv2d."""
     def __init__(self, conv, dtype, device, stream, shuffle=1):
@@ -908,13 +956,9 @@ class DBSREngine:
         if copy:
             pred, offs = pred.clone(), offs.clone()
             fw_t = fw_t.clone() if want_fw else None
-        aux = {'offsets': offs.view(B, N - 1, 2, H, W)}
-        if want_fw:
-            # [B*N,H,W,C] channels-last storage viewed as the reference's [B,N,C,H,W]
-            aux['fusion_weights'] = fw_t.view(B, N, H, W, -1).permute(0, 1, 4, 2, 3)
-        else:
-            aux['fusion_weights'] = None
-        return pred.view(pred.shape), aux
+        # [B*N,H,W,C] channels-last storage viewed as the reference's [B,N,C,H,W]; fp32 NCHW on first read
+        native = fw_t.view(B, N, H, W, -1).permute(0, 1, 4, 2, 3) if want_fw else None
+        return pred.view(pred.shape), DBSRAux(offs.view(B, N - 1, 2, H, W), native)
 
     # ---------------- frame-sharded fusion (BASELINE configs[4]) ----------------
     def decoder_halo(self):

@@ -499,8 +499,8 @@ class DBSRTrainer:
         plan.run_list(plan.ops[:plan.fwd_end], L.stream_ptr(self.dev))
         plan.gen += 1
         B, N, _, H, W = burst.shape
-        fw = plan.FW.t.view(B, N, H, W, -1).permute(0, 1, 4, 2, 3)
-        return plan.bufs['pred'].clone(), plan.bufs['offsets'].view(B, N - 1, 2, H, W).clone(), fw.clone(), \
+        fw = plan.FW.t.clone().view(B, N, H, W, -1).permute(0, 1, 4, 2, 3)
+        return plan.bufs['pred'].clone(), plan.bufs['offsets'].view(B, N - 1, 2, H, W).clone(), fw, \
             (plan, plan.gen)
 
     def backward_from(self, token, gpred):
@@ -597,4 +597,5 @@ def train_forward(net, burst):
     if eng is None or eng.net is not net or eng.dtype != net.compute_dtype:
         eng = net._train_engine = DBSRTrainer(net, optimizer=False)
     pred, offs, fw = _DBSRTrainForward.apply(burst, eng, *eng.params)
-    return pred, {'offsets': offs, 'fusion_weights': fw}
+    from .engine import DBSRAux
+    return pred, DBSRAux(offs, fw)

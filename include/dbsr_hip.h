@@ -321,6 +321,10 @@ int dbsr_adam_step(long long n, float* param, const float* grad, float* exp_avg,
  * dbsr_conv_pack_weights(cout = cin, cin = cout). */
 int dbsr_dgrad_weights(const float* w, int cout, int cin, int kh, int kw, float* wt, void* stream);
 
+/* n NHWC images (c channels from in.c0, any dtype) -> fp32 NCHW out [n][c][hw]: the fusion weights in the
+ * reference's [B,N,C,H,W] fp32 layout (merging.py:117-126), materialised when a caller reads them. */
+int dbsr_nhwc_to_nchw_f32(int n, int hw, int c, dbsr_tensor in, float* out, void* stream);
+
 /* Fill an NHWC slice with zeros (used for channel padding of persistent buffers). */
 int dbsr_zero(void* ptr, size_t bytes, void* stream);
 

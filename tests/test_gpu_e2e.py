@@ -193,3 +193,22 @@ def test_output_slots_zero_copy_and_no_aliasing(synth_sd, use_graph):
             r = ref1 if i % 2 == 0 else ref2
             assert torch.equal(p, r[0]) and torch.equal(o, r[1]['offsets']), i
             assert torch.equal(f, r[1]['fusion_weights']), i
+
+
+def test_fusion_weights_reference_contract(synth_sd):
+    """aux['fusion_weights'] is the reference's tensor (merging.py:117-126): fp32, contiguous [B,N,C,H,W],
+    the softmax over the burst (sums to 1 over N), equal to the engine's channels-last buffer
+    (aux.native_fusion_weights, the zero-copy view) -- in 16-bit compute mode too."""
+    from dbsr_amd.burst import synthetic_bursts
+    burst, _ = synthetic_bursts(2, 5, 32, 48, sr_factor=8, seed=81)
+    net = _net(synth_sd, torch.float16)
+    with torch.no_grad():
+        _, aux = net(burst.to(DEV))
+    fw = aux['fusion_weights']
+    assert fw.dtype == torch.float32 and fw.is_contiguous() and fw.shape == (2, 5, 512, 32, 48)
+    nat = aux.native_fusion_weights
+    assert nat.shape == fw.shape and nat.dtype == torch.float16
+    assert torch.equal(fw, nat.float())
+    s = fw.sum(dim=1)
+    assert float((s - 1).abs().max()) <= 5e-3            # 16-bit stored weights, fp32 softmax
+    assert set(aux.keys()) == {'offsets', 'fusion_weights'} and aux.get('fusion_weights') is fw
