@@ -832,7 +832,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pipe_kernel(ConvK k, int tiles
 
     // tile descriptors hold wave-uniform values only (scalar registers); the lane's own pixel/cout offset
     // within a tile is the same for every tile
-    struct Tile { const T* xf; long long y_off, r_off; int y0, x0, cb; };
+    // EPI 0 only: the training dgrad's ReLU-backward gate (out *= gate > 0), loaded like the residual
+    const bool has_gate = EPI == 0 && k.gt != nullptr;
+    struct Tile { const T* xf; long long y_off, r_off, g_off; int y0, x0, cb; };
     auto decode = [&](int i) {
         int L = i * grid + pb;
         const int ct = L % nct; L /= nct;
@@ -845,8 +847,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pipe_kernel(ConvK k, int tiles
         const long long pix = (long long)t.y0 * k.out_w + t.x0;
         t.y_off = HEAD ? map_frame(k.ym, f) * k.y_is + pix : map_frame(k.ym, f) * k.y_is + k.y_c0 + t.cb + pix * k.y_ld;
         t.r_off = has_res ? map_frame(k.rm, f) * k.r_is + k.r_c0 + t.cb + pix * k.r_ld : 0;
+        t.g_off = has_gate ? map_frame(k.gm, f) * k.g_is + k.g_c0 + t.cb + pix * k.g_ld : 0;
         return t;
     };
+    const long long g_lane = has_gate ? (long long)(wave * C::RPW * k.out_w + col) * k.g_ld + g * 8 : 0;
     const long long y_lane = (long long)(wave * C::RPW * k.out_w + col) * k.y_ld + g * 8;
     const long long r_lane = has_res ? (long long)(wave * C::RPW * k.out_w + col) * k.r_ld + g * 8 : 0;
     // pixel-group jj of a wave = row jj / GPR of its RPW rows, 16-pixel column group jj % GPR
@@ -895,6 +899,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pipe_kernel(ConvK k, int tiles
         for (int j = 0; j < C::GW; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     u32x4_t resv[C::NOUT];              // residual of the tile being computed (loaded in its last stage)
     u32x4_t pend[C::NOUT];              // packed outputs of the last finished tile (stored next stage)
+    u32x4_t gatev[EPI == 0 ? C::NOUT : 1];   // EPI 0 gate of the tile being computed (as resv)
 
     // lane-dependent LDS bases within a stage buffer; tap/fragment offsets are immediates.  Halo pixel
     // P0 + imm of k-group g sits at slot 4(P0 + imm) + halo_phys(P0 + imm, g), and halo_phys depends on
@@ -929,6 +934,16 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pipe_kernel(ConvK k, int tiles
                 for (int e = 0; e < 4; ++e) {
                     v[2 * e] = act2(v[2 * e] + H16<T>::lo(rq[e]));
                     v[2 * e + 1] = act2(v[2 * e + 1] + H16<T>::hi(rq[e]));
+                }
+            }
+            if constexpr (EPI == 0) {
+                if (has_gate) {
+                    const u32x4_t gq = gatev[q];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        v[2 * e] = H16<T>::lo(gq[e]) > 0.f ? v[2 * e] : 0.f;
+                        v[2 * e + 1] = H16<T>::hi(gq[e]) > 0.f ? v[2 * e + 1] : 0.f;
+                    }
                 }
             }
             u32x4_t o;
@@ -1008,6 +1023,14 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pipe_kernel(ConvK k, int tiles
                         resv[q] = *(const u32x4_t*)((const T*)k.r + cur.r_off + r_lane + grp_off(j) * k.r_ld +
                                                     (ok ? 32 * h : 0));
                     }
+                    if constexpr (EPI == 0) {
+                        if (has_gate && last) {
+                            const int h = q / C::GW, j = q % C::GW;
+                            const bool ok = cur.cb + 32 * h + 8 * g < k.cout;
+                            gatev[q] = *(const u32x4_t*)((const T*)k.gt + cur.g_off + g_lane + grp_off(j) * k.g_ld +
+                                                         (ok ? 32 * h : 0));
+                        }
+                    }
                 }
                 if (more) {
 #pragma unroll
@@ -1084,8 +1107,9 @@ int launch_pipe(const ConvK& k, int n_frames, hipStream_t s) {
     int grid = (int)std::min<long long>(nt, cap);
     grid = (grid + 7) / 8 * 8;
     // compile-time epilogues for the forward's three conv flavours, run-time otherwise
-    int epi = 0;
-    if (k.head_cout > 0) epi = 4;
+    int epi = 0;                        // (a gated conv, the training dgrad, takes the run-time epilogue 0)
+    if (k.gt) epi = 0;
+    else if (k.head_cout > 0) epi = 4;
     else if (!k.r && k.act == DBSR_ACT_RELU) epi = 1;
     else if (k.r && k.act == DBSR_ACT_NONE && k.post_act == DBSR_ACT_RELU) epi = 2;
     else if (!k.r && k.act == DBSR_ACT_NONE) epi = 3;
@@ -1114,7 +1138,7 @@ int pick_pipe(const dbsr_conv_desc* d) {
         d->pad != 1 || d->dil != 1 || d->cin <= 16 || d->out_mode != DBSR_OUT_NHWC || d->y.dtype != d->x.dtype)
         return 0;
     if (d->y.ld % 8 || d->y.c0 % 8 || d->cout % 8 || (d->res.ptr && (d->res.ld % 8 || d->res.c0 % 8))) return 0;
-    if (d->gate.ptr) return 0;                                   // gated (backward) convs: tiled/generic kernels
+    if (d->gate.ptr && (d->gate.ld % 8 || d->gate.c0 % 8 || d->gate.dtype != d->y.dtype)) return 0;
     if (cin_pad(d->cin) * 2 + 64 > ZERO_PAGE_BYTES || d->cout > 512) return 0;
     if ((long long)d->in_h * d->in_w * d->x.ld * 2 >= (1LL << 31)) return 0;   // 32-bit buffer offsets per frame
     int cfg = 0, tw = 0, th = 8, wm = 0;
@@ -1196,6 +1220,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ws_kernel(ConvK k, int tiles_x
     const int g = lane >> 4, col = lane & 15;
     const int wc = wave % C::WC, wp = wave / C::WC;
     const bool has_res = EPI == 2 || (EPI == 0 && k.r != nullptr);
+    const bool has_gate = EPI == 0 && k.gt != nullptr;   // training dgrad: out *= (gate > 0)
     auto act1 = [&](float v) {
         if constexpr (EPI == 1) return fmaxf(v, 0.f);
         else if constexpr (EPI == 0) return apply_act(v, k.act);
@@ -1231,7 +1256,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ws_kernel(ConvK k, int tiles_x
     }
     const bool cout_ok = cb + 8 * g < k.cout;
 
-    struct Tile { const T* xf; long long y_off, r_off; int y0, x0; };
+    struct Tile { const T* xf; long long y_off, r_off, g_off; int y0, x0; };
     auto decode = [&](int i) {
         int L = sid + i * S;
         const int tx = L % tiles_x; L /= tiles_x;
@@ -1243,6 +1268,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ws_kernel(ConvK k, int tiles_x
         const long long pix = (long long)t.y0 * k.out_w + t.x0;
         t.y_off = map_frame(k.ym, f) * k.y_is + k.y_c0 + cb + pix * k.y_ld;
         t.r_off = has_res ? map_frame(k.rm, f) * k.r_is : 0;   // residual frame base (buffer-resource base)
+        t.g_off = has_gate ? map_frame(k.gm, f) * k.g_is + k.g_c0 + cb + pix * k.g_ld : 0;
         return t;
     };
     // pixel of group j of this lane, relative to the tile origin
@@ -1288,6 +1314,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ws_kernel(ConvK k, int tiles_x
     };
 
     f32x4_t acc[2][C::GW];
+    u32x4_t gatev[EPI == 0 ? C::GW : 1];
     // residual tile via LDS-DMA: piece q = 64/SPP tile pixels x WM*2 B; lane l -> pixel (64/SPP)q + l/SPP,
     // physical slot l % SPP holding logical slot (l % SPP) ^ (pixel % SPP) -- the XOR keeps the epilogue's
     // ds_read_b128 (16 consecutive pixels x 2 slots per lane group) conflict-free.  Out-of-frame bytes
@@ -1323,11 +1350,25 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ws_kernel(ConvK k, int tiles_x
                     v[2 * e + 1] = act2(v[2 * e + 1] + H16<T>::hi(rq[e]));
                 }
             }
+            if constexpr (EPI == 0) {
+                if (has_gate) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        v[2 * e] = H16<T>::lo(gatev[j][e]) > 0.f ? v[2 * e] : 0.f;
+                        v[2 * e + 1] = H16<T>::hi(gatev[j][e]) > 0.f ? v[2 * e + 1] : 0.f;
+                    }
+                }
+            }
             u32x4_t o;
 #pragma unroll
             for (int e = 0; e < 4; ++e) o[e] = H16<T>::pack(v[2 * e], v[2 * e + 1]);
             if (cout_ok) *(u32x4_t*)((T*)k.y + t.y_off + px_off(j) * k.y_ld + 8 * g) = o;
         }
+    };
+    // EPI 0 gate of a tile into registers during its k-steps (consumed by its epilogue after the next
+    // barrier, whose vmcnt(0) covers the loads); lanes of a partial cout tile past cout read channel cb
+    auto gate_load = [&](const Tile& t, int j) {
+        gatev[j] = *(const u32x4_t*)((const T*)k.gt + t.g_off + px_off(j) * k.g_ld + (cout_ok ? 8 * g : 0));
     };
 
     Tile cur = decode(0), prev = cur;
@@ -1387,6 +1428,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ws_kernel(ConvK k, int tiles_x
                             res_dma(it, nxt, nbuf);
                 }
             }
+            if constexpr (EPI == 0) {
+                if (has_gate && step >= C::STEPS - 1 - C::GW && step < C::STEPS - 1) gate_load(cur, step - (C::STEPS - 1 - C::GW));
+            }
             const int c = step / 9, tap = step % 9;
 #pragma unroll
             for (int j = 0; j < C::GW; ++j) {
@@ -1420,8 +1464,9 @@ inline bool ws_narrow(const dbsr_conv_desc* d) { return d->cout <= 32; }
 int pick_ws(const dbsr_conv_desc* d) {
     if (!g_ws_enabled || !is16(d->x.dtype) || d->precise || d->kh != 3 || d->kw != 3 || d->stride != 1 ||
         d->pad != 1 || d->dil != 1 || d->cin <= 16 || d->cin > 64 || d->out_mode != DBSR_OUT_NHWC ||
-        d->y.dtype != d->x.dtype || d->gate.ptr)
+        d->y.dtype != d->x.dtype)
         return 0;
+    if (d->gate.ptr && (d->gate.ld % 8 || d->gate.c0 % 8 || d->gate.dtype != d->y.dtype)) return 0;
     if (d->y.ld % 8 || d->y.c0 % 8 || d->cout % 8 || d->cout > 512 ||
         (d->res.ptr && (d->res.ld % 8 || d->res.c0 % 8)))
         return 0;
@@ -1445,8 +1490,9 @@ int launch_ws(const ConvK& k, const dbsr_conv_desc* d, int px, hipStream_t s) {
     const int tiles_x = k.out_w / TW, tiles_y = k.out_h / TH;
     const int nct = (k.cout + WM - 1) / WM;
     const int nsp = d->n_frames * tiles_x * tiles_y;
-    int epi = 0;
-    if (!k.r && k.act == DBSR_ACT_RELU) epi = 1;
+    int epi = 0;                        // (a gated conv, the training dgrad, takes the run-time epilogue 0)
+    if (k.gt) epi = 0;
+    else if (!k.r && k.act == DBSR_ACT_RELU) epi = 1;
     else if (k.r && k.act == DBSR_ACT_NONE && k.post_act == DBSR_ACT_RELU) epi = 2;
     else if (!k.r && k.act == DBSR_ACT_NONE) epi = 3;
 #define DBSR_WS_LAUNCH(E)                                                                                         \

@@ -187,6 +187,7 @@ class Plan:
         self.lanes = {0}
         self.streams = {}
         self.max_blocks = 0  # CU cap for lane-0 persistent convs issued while a side lane runs
+        self.max_blocks_cap = 0
 
     def add(self, name, fn, *args, work=None):
         if work is not None:
@@ -320,9 +321,23 @@ class Plan:
             if rc != 0:
                 L.check(rc, name)
 
-    def time_ops(self, stream, reps=10):
+    def time_ops(self, stream, reps=10, full_chip=True):
         """Average device time (ms) of each op, each launched `reps` times back to back between two
-        HIP events on `stream` (all lanes serialised onto it; fork/join entries report 0)."""
+        HIP events on `stream` (all lanes serialised onto it; fork/join entries report 0).
+
+        full_chip: the lane-0 convs that the plan caps to part of the CUs while the PWC-Net lane runs beside
+        them (max_blocks) are timed uncapped, i.e. as kernels on the whole chip -- serialised here, nothing
+        else runs beside them, so a capped time would price the idle CUs into the kernel."""
+        capped = [(d, d.max_blocks) for d, _ in self.convs if d.max_blocks] if full_chip else []
+        for d, _ in capped:
+            d.max_blocks = 0
+        try:
+            return self._time_ops(stream, reps)
+        finally:
+            for d, mb in capped:
+                d.max_blocks = mb
+
+    def _time_ops(self, stream, reps):
         out = []
         for fn, args, name, lane in self.ops:
             if fn is Plan.FORK or fn is Plan.JOIN:
@@ -775,7 +790,7 @@ class DBSREngine:
         plan.fork(1, dev, priority=-1)
         WP = self._emit_flow(plan, grp, N, H, W, sh)          # PWC-Net on lane 1
         plan.switch(0)
-        plan.max_blocks = plan_cap
+        plan.max_blocks = plan.max_blocks_cap = plan_cap
         # ---------------- encoder (encoders.py:66-72), whole batch ----------------
         e = [NHWC(F, H, W, r8(self.enc_init.cout), dt, dev) for _ in range(3)]
         plan.conv('enc.init', self.enc_init, F, raw, 0, hw, e[0], 0, L.ACT_RELU)

@@ -136,6 +136,7 @@ class DBSRTrainer:
         self.step_count = 0
         self.plans = {}
         self.loss = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.use_graph = True         # step(): replay the plan as HIP graphs after its first (eager) run
         self._pack()
 
     def _trainable_convs(self):
@@ -205,7 +206,8 @@ class DBSRTrainer:
             co = tc.cout if cout is None else cout
             need = lib.dbsr_conv_wgrad_workspace_bytes(n, h, w, ci, co, tc.k)
             plan.add('wgrad.' + name, lib.dbsr_conv_wgrad, n, h, w, x.d(xc0, xmap), ci, dy.d(dyc0, dymap), co, tc.k,
-                     tc.gw, accumulate, ws('wg', need), need)
+                     tc.gw, accumulate, ws('wg', need), need, work=('flop', 2.0 * n * h * w * ci * co * tc.k * tc.k))
+            plan.kernel[len(plan.ops) - 1] = 'conv_wgrad'
 
         def bgrad(name, tc, n, hwp, dy, dyc0, c=None, accumulate=0):
             if tc.gb is None:
@@ -433,6 +435,7 @@ class DBSRTrainer:
         plan.bufs = bufs
         plan.buckets = buckets
         plan.FW, plan.gen = FW, 0
+        plan.graphs, plan.eager_runs = None, 0      # HIP graphs of the step's segments (DBSRTrainer.step)
         return plan
 
     # ------------------------------------------------------------------------------------------------
@@ -447,17 +450,30 @@ class DBSRTrainer:
         plan.bufs['burst'].copy_(burst.to(torch.float32), non_blocking=True)
         plan.bufs['gt'].copy_(frame_gt.to(torch.float32), non_blocking=True)
         stream = L.stream_ptr(self.dev)
+        # segments of the op list between the gradient buckets' completion points: each segment is one HIP
+        # graph replay (after one eager step), and a bucket's all-reduce is issued right after its segment
+        cuts = [0] + ([b[0] for b in plan.buckets] if self.world > 1 else []) + [len(plan.ops)]
+        segs = [(a, b) for a, b in zip(cuts[:-1], cuts[1:]) if b > a]
+        if self.use_graph and plan.graphs is None and plan.eager_runs > 0:
+            plan.graphs = []
+            for a, b in segs:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    plan.run_list(plan.ops[a:b], L.stream_ptr(self.dev))
+                plan.graphs.append(g)
         works = []
         bi = 0
-        for i, (fn, args, name, lane) in enumerate(plan.ops):
-            rc = fn(*args, stream)
-            if rc != 0:
-                L.check(rc, name)
-            while bi < len(plan.buckets) and plan.buckets[bi][0] == i + 1:
+        for si, (a, b) in enumerate(segs):
+            if plan.graphs is not None:
+                plan.graphs[si].replay()
+            else:
+                plan.run_list(plan.ops[a:b], stream)
+            while bi < len(plan.buckets) and plan.buckets[bi][0] == b:
                 if self.world > 1:
                     _, lo, hi = plan.buckets[bi]
                     works.append(allreduce_bucket(self.flat_grad, lo, hi, self.pg))
                 bi += 1
+        plan.eager_runs += 1
         for w_ in works:
             w_.wait()
         self.step_count += 1

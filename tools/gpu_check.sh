@@ -20,4 +20,6 @@ timeout -k 10 300 python bench.py --kernel-breakdown > $out/bench_fp16.json 2> $
 cat $out/bench_fp16.json
 timeout -k 10 300 python bench.py --dtype bf16 --no-cpu-baseline > $out/bench_bf16.json 2> $out/bench_bf16.err || { echo bench bf16 failed; exit 1; }
 python -c "import json;d=json.load(open('$out/bench_bf16.json'));print('bf16', d['value'], d['ms_per_step'])"
+timeout -k 10 300 python bench.py --mode train --steps 5 --warmup 2 --kernel-breakdown > $out/bench_train.json 2> $out/bench_train.err || { echo bench train failed; tail -20 $out/bench_train.err; exit 1; }
+python -c "import json;d=json.load(open('$out/bench_train.json'));print('train', d['value'], d['ms_per_step'], d['step_roofline'])"
 echo done

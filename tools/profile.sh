@@ -10,10 +10,10 @@ mkdir -p $out
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace -o run --output-format csv -- \
     python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > $out/bench_trace.log 2>&1 || exit $?
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "warp512|warp_kernel|fuse_softmax|fuse512|conv3x3|conv1x1" \
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "warp512|warp_kernel|fuse_softmax|fuse512|conv3x3|conv1x1|upsample_shuffle|pwc_dense|pwc_extract" \
     -d $out/pmc_fetch -o run --output-format csv -- \
     python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > $out/bench_fetch.log 2>&1 || exit $?
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "warp512|warp_kernel|fuse_softmax|fuse512|conv3x3|conv1x1" \
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "warp512|warp_kernel|fuse_softmax|fuse512|conv3x3|conv1x1|upsample_shuffle|pwc_dense|pwc_extract" \
     -d $out/pmc_write -o run --output-format csv -- \
     python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > $out/bench_write.log 2>&1 || exit $?
 echo done

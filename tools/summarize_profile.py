@@ -8,6 +8,7 @@ own rocprofv3 --pmc pass (no trace domains combined).
 Usage: python tools/summarize_profile.py gpurun_out/prof_r01 r01
 """
 import csv
+import json
 import os
 import shutil
 import statistics
@@ -19,6 +20,37 @@ KERNELS = {   # label -> (name predicate, algorithmic bytes per launch at the de
     'fusion kernel (merging.py:116-126)': (lambda n: 'fuse_softmax_kernel' in n or 'fuse512_bf16_kernel' in n, None),
     'conv3x3_pipe_kernel, largest grid (wp.out 128->512)': (lambda n: 'conv3x3_pipe_kernel<' in n and '64, 48, 8, 3>' in n, None),
 }
+
+
+# kernel name -> bench.py family (bench.py CONV_FAMILIES / roofline_hbm keys)
+FAMILY = [('conv3x3_ws_kernel', 'conv3x3_ws'), ('conv3x3_pipe_kernel', 'conv3x3_pipe'),
+          ('conv3x3_tiled_kernel', 'conv3x3_tiled'), ('conv1x1_kernel', 'conv1x1'),
+          ('upsample_shuffle_kernel', 'conv1x1_shuffle'), ('pwc_dense_kernel', 'pwc_dense'),
+          ('pwc_extract_kernel', 'pwc_extract'), ('warp512_bf16_kernel', 'warp'), ('fuse512_bf16_kernel', 'fuse')]
+
+
+def family(name):
+    for key, fam in FAMILY:
+        if key in name:
+            return fam
+    return None
+
+
+def traffic_json(fetch, write, tag):
+    """profiles/pmc_traffic.json: mean HBM bytes per launch of each kernel family (2 x FETCH_SIZE + WRITE_SIZE,
+    KB units) over every profiled dispatch of the family -- every op of the forward is dispatched equally often
+    in the profiled bench run, so this is the per-launch average over one forward's launches."""
+    out = {}
+    for fam in sorted({family(r['Kernel_Name']) for r in fetch} - {None}):
+        fv = [float(r['Counter_Value']) for r in fetch if family(r['Kernel_Name']) == fam]
+        wv = [float(r['Counter_Value']) for r in write if family(r['Kernel_Name']) == fam]
+        if not fv or not wv:
+            continue
+        fb, wb = 2 * statistics.mean(fv) * 1024, statistics.mean(wv) * 1024
+        out[fam] = {'bytes_per_launch': round(fb + wb), 'fetch_bytes': round(fb), 'write_bytes': round(wb),
+                    'dispatches': len(fv), 'source': 'rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, '
+                    'profiles/%s_summary.md (FETCH_SIZE x2, gfx950)' % tag}
+    return out
 
 
 def main():
@@ -55,6 +87,13 @@ def main():
         wmb = statistics.median(wv) * 1024 / 1e6
         lines.append('| %s | %d | %.1f | %.1f | %.1f | %.1f |' % (label, len(fv), fmb, wmb, fmb + wmb,
                                                                 statistics.median(dur) / 1e3))
+    traffic = traffic_json(fetch, write, tag)
+    lines += ['', '## HBM traffic per launch by kernel family (mean over all profiled dispatches)', '',
+              '| family | dispatches | fetch MB | write MB | traffic/launch MB |', '|---|---|---|---|---|']
+    for fam, t in traffic.items():
+        lines.append('| %s | %d | %.1f | %.1f | %.1f |' % (fam, t['dispatches'], t['fetch_bytes'] / 1e6,
+                                                          t['write_bytes'] / 1e6, t['bytes_per_launch'] / 1e6))
+    json.dump(traffic, open(os.path.join(outdir, 'pmc_traffic.json'), 'w'), indent=1)
     open(os.path.join(outdir, f'{tag}_summary.md'), 'w').write('\n'.join(lines) + '\n')
     print('\n'.join(lines))
 
