@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get('DBSR_HIP_LIB', os.path.join(_HERE, 'libdbsr_hip.so'))
 DBSR_F32, DBSR_BF16, DBSR_F16 = 0, 1, 2
 ACT_NONE, ACT_RELU, ACT_LRELU = 0, 1, 2
 OUT_NHWC, OUT_SHUFFLE, OUT_NCHW_F32 = 0, 1, 2
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 
 class FrameMap(ctypes.Structure):
@@ -121,6 +121,10 @@ def lib():
             'dbsr_warp_backward': ([c_int, c_int, c_int, c_int, Tensor, c_void_p, c_ll, c_void_p, FrameMap, c_ll,
                                     c_void_p], c_int),
             'dbsr_enc_grad_gate': ([c_int, c_int, c_int, c_int, Tensor, c_void_p, Tensor, Tensor, c_void_p], c_int),
+            'dbsr_warp_backward_gather_workspace_bytes': ([c_int, c_int, c_int], c_size_t),
+            'dbsr_warp_backward_gather': ([c_int, c_int, c_int, c_int, Tensor, c_void_p, c_ll, Tensor, Tensor, c_void_p,
+                                           c_size_t, c_void_p], c_int),
+            'dbsr_gate_copy': ([c_int, c_int, c_int, Tensor, Tensor, Tensor, c_void_p], c_int),
             'dbsr_adam_step': ([c_ll, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_float, c_float, c_float, c_int,
                                 c_float, c_void_p], c_int),
             'dbsr_dgrad_weights': ([c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p], c_int),
@@ -157,6 +161,7 @@ EXPORTED = ['dbsr_abi_version', 'dbsr_last_error', 'dbsr_conv_packed_elems', 'db
             'dbsr_merge_prep', 'dbsr_pwc_assemble', 'dbsr_zero', 'dbsr_nhwc_to_nchw_f32', 'dbsr_conv_wgrad_workspace_bytes', 'dbsr_conv_wgrad',
             'dbsr_chan_sum_workspace_bytes', 'dbsr_chan_sum', 'dbsr_l1_loss_backward', 'dbsr_relu_grad', 'dbsr_unshuffle_gate',
             'dbsr_fuse_backward', 'dbsr_merge_prep_backward', 'dbsr_warp_backward', 'dbsr_enc_grad_gate',
+            'dbsr_warp_backward_gather_workspace_bytes', 'dbsr_warp_backward_gather', 'dbsr_gate_copy',
             'dbsr_adam_step', 'dbsr_dgrad_weights',
             'dbsr_resize_bilinear', 'dbsr_gauss_reflect', 'dbsr_color_fit', 'dbsr_color_apply', 'dbsr_pwc_dense',
             'dbsr_pwc_dense_supported', 'dbsr_pwc_extract', 'dbsr_pwc_extract_supported',

@@ -1147,6 +1147,9 @@ int pick_pipe(const dbsr_conv_desc* d) {
     // 16x16 frames (the PWC level-2 DenseNet and the refiner's first conv, pwcnet.py:123-150,188): one whole
     // frame per tile; a tile per block is enough to beat the LDS-tiled kernel on their 128 - 576 channels
     else if (d->cout > 32 && d->out_w == 16 && d->out_h == 16) { cfg = 3; tw = 16; th = 16; wm = 64; }
+    // frame widths that are multiples of 32 but not 48 (the training step's 128x128 frames): 32x16 tiles
+    // (not gated: the run-time epilogue's gate registers spill at this tile)
+    else if (d->cout > 32 && d->out_w % 32 == 0 && d->out_h % 16 == 0 && !d->gate.ptr) { cfg = 4; tw = 32; th = 16; wm = 64; }
     if (!cfg || d->out_h % th) return 0;
     const long long nt = (long long)d->n_frames * (d->out_w / tw) * (d->out_h / th) * ((d->cout + wm - 1) / wm);
     return (nt >= (cfg == 3 ? 64 : 256) || g_pipe_enabled == 2) ? cfg : 0;
@@ -1201,9 +1204,9 @@ template <typename T, int WM, int TW, int TH, int NCH, int EPI>
 __global__ __launch_bounds__(512, 1) void conv3x3_ws_kernel(ConvK k, int tiles_x, int tiles_y, int nct, int nsp,
                                                             int px) {
     using C = WsCfg<WM, TW, TH, NCH>;
-    static_assert(EPI >= 0 && EPI <= 3, "epilogues 0-3");
+    static_assert(EPI >= 0 && EPI <= 5 && EPI != 4, "epilogues 0-3, 5");
     DBSR_OWN_SIMDS();
-    constexpr int RES_BUFS = (EPI == 0 || EPI == 2) ? 2 : 0;
+    constexpr int RES_BUFS = (EPI == 0 || EPI == 2 || EPI == 5) ? 2 : 0;
     // the next tile's halo goes out over the first half of the k-steps when the residual follows in the
     // second half, else over the first two thirds (measured: enc.out 205 -> 196 us, residual convs slower)
     constexpr int DMA_STEPS = RES_BUFS > 0 ? C::DMA_STEPS : (2 * C::STEPS) / 3;
@@ -1219,16 +1222,17 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ws_kernel(ConvK k, int tiles_x
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int g = lane >> 4, col = lane & 15;
     const int wc = wave % C::WC, wp = wave / C::WC;
-    const bool has_res = EPI == 2 || (EPI == 0 && k.r != nullptr);
-    const bool has_gate = EPI == 0 && k.gt != nullptr;   // training dgrad: out *= (gate > 0)
+    // EPI 5: EPI 0 plus the training dgrad's gate, out *= (gate > 0), loaded at the start of the epilogue
+    const bool has_res = EPI == 2 || ((EPI == 0 || EPI == 5) && k.r != nullptr);
+    const bool has_gate = EPI == 5;
     auto act1 = [&](float v) {
         if constexpr (EPI == 1) return fmaxf(v, 0.f);
-        else if constexpr (EPI == 0) return apply_act(v, k.act);
+        else if constexpr (EPI == 0 || EPI == 5) return apply_act(v, k.act);
         else return v;
     };
     auto act2 = [&](float v) {
         if constexpr (EPI == 2) return fmaxf(v, 0.f);
-        else if constexpr (EPI == 0) return apply_act(v, k.post_act);
+        else if constexpr (EPI == 0 || EPI == 5) return apply_act(v, k.post_act);
         else return v;
     };
 
@@ -1314,7 +1318,6 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ws_kernel(ConvK k, int tiles_x
     };
 
     f32x4_t acc[2][C::GW];
-    u32x4_t gatev[EPI == 0 ? C::GW : 1];
     // residual tile via LDS-DMA: piece q = 64/SPP tile pixels x WM*2 B; lane l -> pixel (64/SPP)q + l/SPP,
     // physical slot l % SPP holding logical slot (l % SPP) ^ (pixel % SPP) -- the XOR keeps the epilogue's
     // ds_read_b128 (16 consecutive pixels x 2 slots per lane group) conflict-free.  Out-of-frame bytes
@@ -1330,6 +1333,13 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ws_kernel(ConvK k, int tiles_x
         blds16(buf_rsrc((const T*)k.r + t.r_off, rframe_bytes), off, 0, lres + buf * C::RES_U4 + q * 64);
     };
     auto epilogue = [&](const Tile& t, int rbuf) {
+        u32x4_t gatev[EPI == 5 ? C::GW : 1];
+        if constexpr (EPI == 5) {
+            // lanes of a partial cout tile past cout read channel cb (never stored)
+#pragma unroll
+            for (int j = 0; j < C::GW; ++j)
+                gatev[j] = *(const u32x4_t*)((const T*)k.gt + t.g_off + px_off(j) * k.g_ld + (cout_ok ? 8 * g : 0));
+        }
         const float4 b0 = *(const float4*)(lbias + wc * 32 + 8 * g);
         const float4 b1 = *(const float4*)(lbias + wc * 32 + 8 * g + 4);
         const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
@@ -1350,13 +1360,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ws_kernel(ConvK k, int tiles_x
                     v[2 * e + 1] = act2(v[2 * e + 1] + H16<T>::hi(rq[e]));
                 }
             }
-            if constexpr (EPI == 0) {
-                if (has_gate) {
+            if constexpr (EPI == 5) {
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        v[2 * e] = H16<T>::lo(gatev[j][e]) > 0.f ? v[2 * e] : 0.f;
-                        v[2 * e + 1] = H16<T>::hi(gatev[j][e]) > 0.f ? v[2 * e + 1] : 0.f;
-                    }
+                for (int e = 0; e < 4; ++e) {
+                    v[2 * e] = H16<T>::lo(gatev[j][e]) > 0.f ? v[2 * e] : 0.f;
+                    v[2 * e + 1] = H16<T>::hi(gatev[j][e]) > 0.f ? v[2 * e + 1] : 0.f;
                 }
             }
             u32x4_t o;
@@ -1364,11 +1372,6 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ws_kernel(ConvK k, int tiles_x
             for (int e = 0; e < 4; ++e) o[e] = H16<T>::pack(v[2 * e], v[2 * e + 1]);
             if (cout_ok) *(u32x4_t*)((T*)k.y + t.y_off + px_off(j) * k.y_ld + 8 * g) = o;
         }
-    };
-    // EPI 0 gate of a tile into registers during its k-steps (consumed by its epilogue after the next
-    // barrier, whose vmcnt(0) covers the loads); lanes of a partial cout tile past cout read channel cb
-    auto gate_load = [&](const Tile& t, int j) {
-        gatev[j] = *(const u32x4_t*)((const T*)k.gt + t.g_off + px_off(j) * k.g_ld + (cout_ok ? 8 * g : 0));
     };
 
     Tile cur = decode(0), prev = cur;
@@ -1427,9 +1430,6 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ws_kernel(ConvK k, int tiles_x
                         if (DMA_STEPS + (it * (C::STEPS - 2 - DMA_STEPS)) / C::RPER == step)
                             res_dma(it, nxt, nbuf);
                 }
-            }
-            if constexpr (EPI == 0) {
-                if (has_gate && step >= C::STEPS - 1 - C::GW && step < C::STEPS - 1) gate_load(cur, step - (C::STEPS - 1 - C::GW));
             }
             const int c = step / 9, tap = step % 9;
 #pragma unroll
@@ -1490,8 +1490,8 @@ int launch_ws(const ConvK& k, const dbsr_conv_desc* d, int px, hipStream_t s) {
     const int tiles_x = k.out_w / TW, tiles_y = k.out_h / TH;
     const int nct = (k.cout + WM - 1) / WM;
     const int nsp = d->n_frames * tiles_x * tiles_y;
-    int epi = 0;                        // (a gated conv, the training dgrad, takes the run-time epilogue 0)
-    if (k.gt) epi = 0;
+    int epi = 0;                        // (a gated conv, the training dgrad, takes epilogue 5)
+    if (k.gt) epi = 5;
     else if (!k.r && k.act == DBSR_ACT_RELU) epi = 1;
     else if (k.r && k.act == DBSR_ACT_NONE && k.post_act == DBSR_ACT_RELU) epi = 2;
     else if (!k.r && k.act == DBSR_ACT_NONE) epi = 3;
@@ -1502,6 +1502,7 @@ int launch_ws(const ConvK& k, const dbsr_conv_desc* d, int px, hipStream_t s) {
         case 1: DBSR_WS_LAUNCH(1); break;
         case 2: DBSR_WS_LAUNCH(2); break;
         case 3: DBSR_WS_LAUNCH(3); break;
+        case 5: DBSR_WS_LAUNCH(5); break;
         default: DBSR_WS_LAUNCH(0); break;
     }
 #undef DBSR_WS_LAUNCH
@@ -1520,6 +1521,7 @@ template <typename T>
 int dispatch_pipe(int cfg, const ConvK& k, const dbsr_conv_desc* d, hipStream_t s) {
     if (cfg == 1) return launch_pipe<T, 64, 48, 8>(k, d->n_frames, s);
     if (cfg == 3) return launch_pipe<T, 64, 16, 16>(k, d->n_frames, s);
+    if (cfg == 4) return launch_pipe<T, 64, 32, 16>(k, d->n_frames, s);
     return launch_pipe<T, 32, 64, 8>(k, d->n_frames, s);
 }
 
@@ -1780,8 +1782,8 @@ int launch_upsample(const ConvK& k, hipStream_t s) {
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ int pw_key(int c) { return (c & 3) | ((c >> 1) & 12); }
 
-template <typename T, int CT, int KS, int PG, int NW>
-__global__ __launch_bounds__(NW * 64, PG == 1 ? 4 : 2) void conv1x1_kernel(ConvK k, int ngroups) {
+template <typename T, int CT, int KS, int PG, int NW, int RES>
+__global__ __launch_bounds__(NW * 64, CT > 2 ? 1 : (PG == 1 ? 4 : 2)) void conv1x1_kernel(ConvK k, int ngroups) {
     constexpr int KQ = KS * 4;                            // 16-B chunks per weight row
     __shared__ __attribute__((aligned(16))) u32x4_t pw_lds[CT * 32 * KQ];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1792,11 +1794,14 @@ __global__ __launch_bounds__(NW * 64, PG == 1 ? 4 : 2) void conv1x1_kernel(ConvK
     }
     __syncthreads();
     const int hw = k.out_h * k.out_w;
-    f32x4_t bias[CT][2];
+    constexpr bool HOIST = CT <= 2;                       // bias in registers across pixel groups (projections)
+    f32x4_t bias[HOIST ? CT : 1][2];
+    if constexpr (HOIST) {
 #pragma unroll
-    for (int ct = 0; ct < CT; ++ct)
+        for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
-        for (int h = 0; h < 2; ++h) bias[ct][h] = load_bias4(k, ct * 32 + 8 * g + 4 * h);
+            for (int h = 0; h < 2; ++h) bias[ct][h] = load_bias4(k, ct * 32 + 8 * g + 4 * h);
+    }
     for (int grp = blockIdx.x * NW + wave; grp < ngroups; grp += gridDim.x * NW) {
         Frag<T> b[PG][KS];
         int pf[PG], prr[PG];
@@ -1814,7 +1819,8 @@ __global__ __launch_bounds__(NW * 64, PG == 1 ? 4 : 2) void conv1x1_kernel(ConvK
                 else b[j][ks].zero();
             }
         }
-#pragma unroll
+        constexpr int CTU = CT <= 2 ? CT : 1;             // (wide couts: one 32-cout tile at a time)
+#pragma unroll CTU
         for (int ct = 0; ct < CT; ++ct) {
             f32x4_t acc[2][PG];
 #pragma unroll
@@ -1833,16 +1839,29 @@ __global__ __launch_bounds__(NW * 64, PG == 1 ? 4 : 2) void conv1x1_kernel(ConvK
                     for (int j = 0; j < PG; ++j) acc[h][j] = mma(a, b[j][ks], acc[h][j]);
                 }
             }
+            f32x4_t bv[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) bv[h] = HOIST ? bias[HOIST ? ct : 0][h] : load_bias4(k, ct * 32 + 8 * g + 4 * h);
 #pragma unroll
             for (int j = 0; j < PG; ++j) {
                 if (pf[j] < 0) continue;
-                u32x4_t o;
+                float v[8];
 #pragma unroll
                 for (int h = 0; h < 2; ++h)
 #pragma unroll
-                    for (int e = 0; e < 2; ++e)
-                        o[2 * h + e] = H16<T>::pack(apply_act(acc[h][j][2 * e] + bias[ct][h][2 * e], k.act),
-                                                    apply_act(acc[h][j][2 * e + 1] + bias[ct][h][2 * e + 1], k.act));
+                    for (int e = 0; e < 4; ++e) v[4 * h + e] = apply_act(acc[h][j][e] + bv[h][e], k.act);
+                if constexpr (RES) {                      // (training dgrad of the projection: + residual, post-act)
+                    const u32x4_t rq = *(const u32x4_t*)((const T*)k.r + map_frame(k.rm, pf[j]) * k.r_is +
+                                                          (long long)prr[j] * k.r_ld + k.r_c0 + ct * 32 + 8 * g);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        v[2 * e] = apply_act(v[2 * e] + H16<T>::lo(rq[e]), k.post_act);
+                        v[2 * e + 1] = apply_act(v[2 * e + 1] + H16<T>::hi(rq[e]), k.post_act);
+                    }
+                }
+                u32x4_t o;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) o[e] = H16<T>::pack(v[2 * e], v[2 * e + 1]);
                 *(u32x4_t*)((T*)k.y + map_frame(k.ym, pf[j]) * k.y_is + (long long)prr[j] * k.y_ld + k.y_c0 + ct * 32 +
                             8 * g) = o;
             }
@@ -1851,9 +1870,12 @@ __global__ __launch_bounds__(NW * 64, PG == 1 ? 4 : 2) void conv1x1_kernel(ConvK
 }
 
 bool use_pointwise(const dbsr_conv_desc* d) {
+    const int ct = d->cout / 32;
     return is16(d->x.dtype) && d->y.dtype == d->x.dtype && !d->precise && d->out_mode == DBSR_OUT_NHWC &&
-           !d->res.ptr && !d->gate.ptr && d->kh == 1 && d->kw == 1 && d->stride == 1 && d->pad == 0 &&
-           d->cin % 32 == 0 && d->cin <= 512 && ((d->cin / 32) & (d->cin / 32 - 1)) == 0 && (d->cout == 32 || d->cout == 64) && d->cout * d->cin <= 32768 &&
+           (!d->res.ptr || (d->res.dtype == d->y.dtype && d->res.ld % 8 == 0 && d->res.c0 % 8 == 0)) &&
+           !d->gate.ptr && d->kh == 1 && d->kw == 1 && d->stride == 1 && d->pad == 0 &&
+           d->cin % 32 == 0 && d->cin <= 512 && ((d->cin / 32) & (d->cin / 32 - 1)) == 0 && d->cout % 32 == 0 &&
+           ct >= 1 && ct <= 16 && (ct & (ct - 1)) == 0 && d->cout * d->cin <= 32768 &&
            d->y.ld % 8 == 0 && d->y.c0 % 8 == 0 && g_tiled_enabled &&
            (long long)d->n_frames * d->out_h * d->out_w >= 4096;
 }
@@ -1864,11 +1886,16 @@ int launch_pointwise_cfg(const ConvK& k, hipStream_t s) {
     const int ks = k.Kp / 32;
     const int lds = CT * 32 * k.Kp * 2;                 // bytes of the block's weight copy
     const unsigned grid = (unsigned)std::min((ngroups + NW - 1) / NW, 256 * (lds <= 40960 ? 3 : 2));
+    // (weight copies up to 64 KiB: CT * KS <= 32; use_pointwise admits only those)
 #define DBSR_PW(KS) \
-    if (ks == KS) { hipLaunchKernelGGL((conv1x1_kernel<T, CT, KS, PG, NW>), dim3(grid), dim3(NW * 64), 0, s, k, ngroups); }
+    if constexpr (CT * KS <= 32) { \
+        if (ks == KS) { \
+            if (k.r) hipLaunchKernelGGL((conv1x1_kernel<T, CT, KS, PG, NW, 1>), dim3(grid), dim3(NW * 64), 0, s, k, ngroups); \
+            else hipLaunchKernelGGL((conv1x1_kernel<T, CT, KS, PG, NW, 0>), dim3(grid), dim3(NW * 64), 0, s, k, ngroups); } }
     DBSR_PW(1) DBSR_PW(2) DBSR_PW(4) DBSR_PW(8) DBSR_PW(16)
 #undef DBSR_PW
-    DBSR_CHECK_ARG(ks == 1 || ks == 2 || ks == 4 || ks == 8 || ks == 16, "conv1x1: cin %d not 32/64/128/256/512", k.Kp);
+    DBSR_CHECK_ARG((ks == 1 || ks == 2 || ks == 4 || ks == 8 || ks == 16) && CT * ks <= 32,
+                   "conv1x1: cin %d x cout %d not served", k.Kp, CT * 32);
     DBSR_LAUNCH_CHECK();
     return 0;
 }
@@ -1882,7 +1909,13 @@ int launch_pointwise_ct(const ConvK& k, hipStream_t s) {
 
 template <typename T>
 int launch_pointwise(const ConvK& k, hipStream_t s) {
-    return k.cout == 64 ? launch_pointwise_ct<T, 2>(k, s) : launch_pointwise_ct<T, 1>(k, s);
+    switch (k.cout / 32) {
+        case 16: return launch_pointwise_ct<T, 16>(k, s);   // (training: dgrad of the 512 -> 64 projection)
+        case 8: return launch_pointwise_ct<T, 8>(k, s);
+        case 4: return launch_pointwise_ct<T, 4>(k, s);
+        case 2: return launch_pointwise_ct<T, 2>(k, s);
+        default: return launch_pointwise_ct<T, 1>(k, s);
+    }
 }
 
 ConvK make_convk(const dbsr_conv_desc* d) {

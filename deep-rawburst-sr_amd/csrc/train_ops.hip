@@ -15,7 +15,7 @@ namespace {
 
 inline unsigned nblocks(long long total, int bs) { return (unsigned)((total + bs - 1) / bs); }
 bool map_ok(const dbsr_tensor& t) { return t.ptr && t.map.fpg > 0; }
-bool vec_ok(const dbsr_tensor& t, int v) { return t.ld % v == 0 && t.c0 % v == 0; }
+__host__ __device__ inline bool vec_ok(const dbsr_tensor& t, int v) { return t.ld % v == 0 && t.c0 % v == 0; }
 
 template <typename F>
 int by_dtype(int dtype, F&& f) {
@@ -42,12 +42,13 @@ int by_dtype(int dtype, F&& f) {
 // [block][wave][co][ci]; wgrad_reduce sums the slots in a fixed order (deterministic).
 // ------------------------------------------------------------------------------------------------
 constexpr int WG_TH = 8, WG_TW = 16, WG_PX = WG_TH * WG_TW;             // output tile
+// blocks over all (co, ci) tiles, each one fp32 partial slot: one per CU for 64-channel blocks (160+ VGPRs x 9
+// waves), two for 32-channel blocks (97 VGPRs)
+inline int wg_blocks(int cb) { return cb == 32 ? 512 : 256; }
 constexpr int WG_HH = WG_TH + 2, WG_HW = WG_TW + 2, WG_HPX = WG_HH * WG_HW;   // halo
 
-template <typename T> struct WgCfg;
-template <> struct WgCfg<bf16_t> { static constexpr int ROWB = 144; };      // 128 B + 16 B skew per pixel row
-template <> struct WgCfg<f16_t> { static constexpr int ROWB = 144; };
-template <> struct WgCfg<float> { static constexpr int ROWB = 272; };       // 256 B + 16 B
+// a pixel row of CB channels in the LDS: CB elements + 16 B skew
+template <typename T, int CB> struct WgCfg { static constexpr int ROWB = CB * (int)sizeof(T) + 16; };
 
 typedef short v4s_t __attribute__((ext_vector_type(4)));
 struct FragB { bf16x8_t v; };
@@ -66,52 +67,73 @@ __device__ __forceinline__ v4s_t tr16(const unsigned char* lds_byte) {
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s_t*)lds_byte);
 }
 
-template <typename T, int K>
+// CB: the (co, ci) block edge, 64 or 32 (32: the 32-channel convs, whose few MFMAs per tile leave the loop
+// latency-bound -- two tiles are prefetched and the smaller accumulator set leaves room for them)
+template <typename T, int K, int CB>
 __global__ __launch_bounds__(K == 3 ? 576 : 256) void conv_wgrad_kernel(
         int n_frames, int h, int w, dbsr_tensor x, int cin, dbsr_tensor dy, int cout, long long n_units,
         float* __restrict__ partial) {
     constexpr int NW = K == 3 ? 9 : 4;
-    constexpr int ROWB = WgCfg<T>::ROWB;
+    constexpr int NB = CB / 16;                        // 16-channel MFMA blocks per edge
+    constexpr int ROWB = WgCfg<T, CB>::ROWB;
     __shared__ __attribute__((aligned(16))) unsigned char lds[(WG_PX + WG_HPX) * ROWB];
-    unsigned char* ldy = lds;                          // [128 px][64 co]
-    unsigned char* lx = lds + WG_PX * ROWB;            // [180 halo px][64 ci]
+    unsigned char* ldy = lds;                          // [128 px][CB co]
+    unsigned char* lx = lds + WG_PX * ROWB;            // [180 halo px][CB ci]
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int co0 = blockIdx.y * 64, ci0 = blockIdx.z * 64;
+    const int co0 = blockIdx.y * CB, ci0 = blockIdx.z * CB;
     const int tiles_x = (w + WG_TW - 1) / WG_TW, tiles_y = (h + WG_TH - 1) / WG_TH;
     const long long u0 = n_units * blockIdx.x / gridDim.x, u1 = n_units * (blockIdx.x + 1) / gridDim.x;
     const int ky = K == 3 ? wave / 3 : 1, kx = K == 3 ? wave % 3 : 1;   // 1x1: centre "tap"
-    f32x4_t acc[4][4];
+    f32x4_t acc[NB][NB];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < NB; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < NB; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    // 16-channel MFMA blocks that hold any of cout / cin (block-uniform: the rest multiply zeros)
+    const int ni = min(NB, (cout - co0 + 15) / 16), nj = min(NB, (cin - ci0 + 15) / 16);
     constexpr int EPP = 16 / (int)sizeof(T);           // elements per 16-B piece
-    constexpr int PPR = 64 / EPP;                      // pieces per 64-channel row
-    for (long long u = u0; u < u1; ++u) {
+    constexpr int PPR = CB / EPP;                      // pieces per CB-channel row
+    constexpr int PIECES = (WG_PX + WG_HPX) * PPR;
+    constexpr int PT = (PIECES + NW * 64 - 1) / (NW * 64);   // pieces per thread per tile
+    // the next tile's dY / X pieces are loaded into registers while this tile's MFMAs run (software pipeline),
+    // then written to the LDS after the barrier that ends them
+    constexpr int DIST = CB == 32 ? 2 : 1;             // prefetch distance in tiles (register budget)
+    u32x4_t pre[DIST][PT];
+    auto fetch = [&](long long u, u32x4_t (&dst)[PT]) {
         const int tx = (int)(u % tiles_x);
-        long long r = u / tiles_x;
+        const long long r = u / tiles_x;
         const int ty = (int)(r % tiles_y);
         const int f = (int)(r / tiles_y);
         const int y0 = ty * WG_TH, x0 = tx * WG_TW;
-        // ---- stage dY tile and X halo (zeros outside the frame and past cout / cin) ----
         const T* dyf = img_ptr<T>(dy, f);
         const T* xf = img_ptr<T>(x, f);
-        for (int it = threadIdx.x; it < (WG_PX + WG_HPX) * PPR; it += NW * 64) {
+#pragma unroll
+        for (int k = 0; k < PT; ++k) {
+            const int it = threadIdx.x + k * NW * 64;
             const int row = it / PPR, pc = it % PPR;
             u32x4_t v = {0u, 0u, 0u, 0u};
             if (row < WG_PX) {
                 const int yy = y0 + row / WG_TW, xx = x0 + row % WG_TW, c = co0 + pc * EPP;
                 if (yy < h && xx < w && c < cout) v = *(const u32x4_t*)(dyf + ((long long)yy * w + xx) * dy.ld + c);
-                *(u32x4_t*)(ldy + row * ROWB + pc * 16) = v;
-            } else {
+            } else if (it < PIECES) {
                 const int hr = row - WG_PX;
                 const int yy = y0 - 1 + hr / WG_HW, xx = x0 - 1 + hr % WG_HW, c = ci0 + pc * EPP;
                 if ((unsigned)yy < (unsigned)h && (unsigned)xx < (unsigned)w && c < cin)
                     v = *(const u32x4_t*)(xf + ((long long)yy * w + xx) * x.ld + c);
-                *(u32x4_t*)(lx + hr * ROWB + pc * 16) = v;
             }
+            dst[k] = v;
         }
-        __syncthreads();
+    };
+    auto put = [&](const u32x4_t (&src)[PT]) {
+#pragma unroll
+        for (int k = 0; k < PT; ++k) {
+            const int it = threadIdx.x + k * NW * 64;
+            if (it >= PIECES) break;
+            const int row = it / PPR, pc = it % PPR;
+            *(u32x4_t*)(lds + row * ROWB + pc * 16) = src[k];   // ldy rows, then the lx rows right after them
+        }
+    };
+    auto compute = [&]() {
         // ---- MFMAs ----
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
@@ -120,7 +142,7 @@ __global__ __launch_bounds__(K == 3 ? 576 : 256) void conv_wgrad_kernel(
                 // lane (g = lane>>4, q = (lane>>2)&3, p = lane&3): rows k = 8g+q (+4) of this k-step,
                 // channels 4p..4p+3 of each 16-channel block
                 const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-                FragB a[4], b[4];
+                FragB a[NB], b[NB];
 #pragma unroll
                 for (int half = 0; half < 2; ++half) {
                     const int kk = 8 * g + 4 * half + q;             // pixel of the k-step, 0..31
@@ -128,7 +150,7 @@ __global__ __launch_bounds__(K == 3 ? 576 : 256) void conv_wgrad_kernel(
                     const unsigned char* arow = ldy + (ty_ * WG_TW + tx_) * ROWB;
                     const unsigned char* brow = lx + ((ty_ + ky) * WG_HW + tx_ + kx) * ROWB;
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) {
+                    for (int i = 0; i < NB; ++i) {
                         const v4s_t va = tr16(arow + (i * 16 + 4 * p) * 2);
                         const v4s_t vb = tr16(brow + (i * 16 + 4 * p) * 2);
 #pragma unroll
@@ -139,9 +161,10 @@ __global__ __launch_bounds__(K == 3 ? 576 : 256) void conv_wgrad_kernel(
                     }
                 }
 #pragma unroll
-                for (int i = 0; i < 4; ++i)
+                for (int i = 0; i < NB; ++i)
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) acc[i][j] = mma16<T>(a[i], b[j], acc[i][j]);
+                    for (int j = 0; j < NB; ++j)
+                        if (i < ni && j < nj) acc[i][j] = mma16<T>(a[i], b[j], acc[i][j]);
             } else {
                 // fp32: 8 MFMAs of k = 4 pixels; lane (kq = lane>>4, m = lane&15)
                 const int kq = lane >> 4, m = lane & 15;
@@ -151,52 +174,84 @@ __global__ __launch_bounds__(K == 3 ? 576 : 256) void conv_wgrad_kernel(
                     const int ty_ = 2 * s + kk / 16, tx_ = kk % 16;
                     const float* arow = (const float*)(ldy + (ty_ * WG_TW + tx_) * ROWB);
                     const float* brow = (const float*)(lx + ((ty_ + ky) * WG_HW + tx_ + kx) * ROWB);
-                    float av[4], bv[4];
+                    float av[NB], bv[NB];
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) {
+                    for (int i = 0; i < NB; ++i) {
                         av[i] = arow[i * 16 + m];
                         bv[i] = brow[i * 16 + m];
                     }
 #pragma unroll
-                    for (int i = 0; i < 4; ++i)
+                    for (int i = 0; i < NB; ++i)
 #pragma unroll
-                        for (int j = 0; j < 4; ++j)
+                        for (int j = 0; j < NB; ++j)
                             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
                 }
             }
         }
-        __syncthreads();
+    };
+#pragma unroll
+    for (int d = 0; d < DIST; ++d)
+        if (u0 + d < u1) fetch(u0 + d, pre[d]);
+    for (long long u = u0; u < u1; u += DIST) {
+#pragma unroll
+        for (int d = 0; d < DIST; ++d) {
+            if (u + d >= u1) break;
+            put(pre[d]);
+            __syncthreads();
+            if (u + d + DIST < u1) fetch(u + d + DIST, pre[d]);
+            compute();
+            __syncthreads();
+        }
     }
     // ---- this wave's partial: C[m = co][n = ci], lane holds co 4(lane>>4)+r of block i, ci lane&15 of block j
     float* out = partial + ((long long)blockIdx.x * gridDim.y * gridDim.z + blockIdx.y * gridDim.z + blockIdx.z) *
-                               (NW * 64 * 64) + wave * 64 * 64;
+                               (NW * CB * CB) + wave * CB * CB;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < NB; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < NB; ++j)
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-                out[(i * 16 + 4 * (lane >> 4) + r) * 64 + j * 16 + (lane & 15)] = acc[i][j][r];
+                out[(i * 16 + 4 * (lane >> 4) + r) * CB + j * 16 + (lane & 15)] = acc[i][j][r];
 }
 
-// dW[co][ci][tap] (+)= sum over blocks (and, for 1x1, over the 4 waves) of the partial slots
-__global__ void wgrad_reduce_kernel(int nbx, int nty, int ntz, int nw, int taps, int cout, int cin,
-                                    const float* __restrict__ partial, float* __restrict__ dw, int accumulate) {
-    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= (long long)cout * cin * taps) return;
-    const int tap = (int)(idx % taps);
-    const int ci = (int)((idx / taps) % cin), co = (int)(idx / ((long long)taps * cin));
-    const int by = co / 64, bz = ci / 64, cl = co % 64, il = ci % 64;
+// dW[co][ci][tap] (+)= sum over blocks (and, for 1x1, over the 4 waves) of the partial slots.  A block owns
+// (co, tap, 64 consecutive ci) and splits the blocks bx over 4 waves (each wave's loads: 64 consecutive
+// floats); the 4 wave sums are added in a fixed order (deterministic).
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(int nbx, int nty, int ntz, int nw, int taps, int cout,
+                                                           int cin, int cb, const float* __restrict__ partial,
+                                                           float* __restrict__ dw, int accumulate) {
+    const int nci64 = (cin + 63) / 64;
+    int b = blockIdx.x;
+    const int cib = b % nci64;
+    b /= nci64;
+    const int tap = b % taps, co = b / taps;
+    const int il = threadIdx.x & 63, sl = threadIdx.x >> 6;
+    const int ci = cib * 64 + il;
+    const int by = co / cb, cl = co % cb, bz = ci / cb, il_ = ci % cb;
+    const int wsz = cb * cb;
     float s = 0.f;
-    for (int bx = 0; bx < nbx; ++bx) {
-        const float* blk = partial + ((long long)bx * nty * ntz + by * ntz + bz) * (nw * 64 * 64);
-        if (taps == 1) {
-            for (int wv = 0; wv < nw; ++wv) s += blk[wv * 4096 + cl * 64 + il];
-        } else {
-            s += blk[tap * 4096 + cl * 64 + il];
+    if (ci < cin) {
+        const long long slot = (long long)nw * wsz;
+        const float* base = partial + ((long long)by * ntz + bz) * slot + cl * cb + il_;
+#pragma unroll 8
+        for (int bx = sl; bx < nbx; bx += 4) {
+            const float* blk = base + (long long)bx * nty * ntz * slot;
+            if (taps == 1) {
+                for (int wv = 0; wv < nw; ++wv) s += blk[wv * wsz];
+            } else {
+                s += blk[tap * wsz];
+            }
         }
     }
-    dw[idx] = accumulate ? dw[idx] + s : s;
+    __shared__ float red[4][64];
+    red[sl][il] = s;
+    __syncthreads();
+    if (sl == 0 && ci < cin) {
+        const float t = ((red[0][il] + red[1][il]) + red[2][il]) + red[3][il];
+        const long long idx = ((long long)co * cin + ci) * taps + tap;
+        dw[idx] = accumulate ? dw[idx] + t : t;
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -222,14 +277,82 @@ __global__ __launch_bounds__(256) void chan_sum_kernel(int n, int hw, int c, dbs
     if (sub == 0 && ch < c) partial[(long long)blockIdx.x * c + ch] = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
 }
 
-__global__ void sum_rows_kernel(int rows, int c, const float* __restrict__ partial, float* __restrict__ out,
-                                int accumulate, float scale) {
-    const int ch = blockIdx.x * blockDim.x + threadIdx.x;
-    if (ch >= c) return;
+// 16-B version: TPP threads cover a pixel's channel groups of 8 (TPP a power of two >= ceil(c/8)), 256/TPP
+// pixels per block step, four pixel loads in flight per thread; partials [nblk][c] as chan_sum_kernel
+template <typename T, int TPP>
+__global__ __launch_bounds__(256) void chan_sum16_kernel(int n, int hw, int c, dbsr_tensor t, int px_per_block,
+                                                         float* __restrict__ partial) {
+    constexpr int PPI = 256 / TPP;
+    const int cg = threadIdx.x % TPP, row = threadIdx.x / TPP;
+    const bool live = cg * 8 < c;
+    const long long total = (long long)n * hw;
+    const long long p0 = (long long)blockIdx.x * px_per_block, p1 = std::min<long long>(p0 + px_per_block, total);
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (live) {
+        for (long long p = p0 + row; p < p1; p += 4 * PPI) {
+            float v[4][8];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const long long q = p + (long long)u * PPI;
+                if (q < p1) {
+                    const int f = (int)(q / hw), rr = (int)(q - (long long)f * hw);
+                    load8(img_ptr<T>(t, f) + (long long)rr * t.ld + cg * 8, v[u]);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) v[u][j] = 0.f;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) s[j] += v[u][j];
+        }
+    }
+    __shared__ float red[PPI][TPP * 8 + 1];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[row][cg * 8 + j] = s[j];
+    __syncthreads();
+    for (int ch = threadIdx.x; ch < c; ch += 256) {
+        float a = 0.f;
+        for (int r = 0; r < PPI; ++r) a += red[r][ch];
+        partial[(long long)blockIdx.x * c + ch] = a;
+    }
+}
+
+// out[ch] (+)= scale * sum over rows of partial[row][ch]: a block per 64 channels, the rows split over 4 waves
+// (loads of 64 consecutive floats), the 4 wave sums added in a fixed order (deterministic)
+__global__ __launch_bounds__(256) void sum_rows_kernel(int rows, int c, const float* __restrict__ partial,
+                                                       float* __restrict__ out, int accumulate, float scale) {
+    const int il = threadIdx.x & 63, sl = threadIdx.x >> 6;
+    const int ch = blockIdx.x * 64 + il;
     float s = 0.f;
-    for (int r = 0; r < rows; ++r) s += partial[(long long)r * c + ch];
-    s *= scale;
-    out[ch] = accumulate ? out[ch] + s : s;
+    if (ch < c) {
+#pragma unroll 8
+        for (int r = sl; r < rows; r += 4) s += partial[(long long)r * c + ch];
+    }
+    __shared__ float red[4][64];
+    red[sl][il] = s;
+    __syncthreads();
+    if (sl == 0 && ch < c) {
+        const float t = (((red[0][il] + red[1][il]) + red[2][il]) + red[3][il]) * scale;
+        out[ch] = accumulate ? out[ch] + t : t;
+    }
+}
+
+// *out = scale * sum of n partials (one block; strided per-thread sums, then a fixed-order tree)
+__global__ __launch_bounds__(256) void sum_all_kernel(int n, const float* __restrict__ partial, float* __restrict__ out,
+                                                      float scale) {
+    float s = 0.f;
+#pragma unroll 8
+    for (int i = threadIdx.x; i < n; i += 256) s += partial[i];
+    __shared__ float red[256];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int st = 128; st > 0; st >>= 1) {
+        if ((int)threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *out = red[0] * scale;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -274,6 +397,43 @@ __global__ __launch_bounds__(256) void l1_loss_bwd_kernel(int B, int C, int H, i
     if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
 }
 
+// Same, 16-bit dpre with exactly 8 channels per pixel (c0 0, C <= 8): 4 pixels per thread, one 16-B store
+// per pixel (channels C..7 written as the zeros they hold), wave-shuffle partial sums
+template <typename T>
+__global__ __launch_bounds__(256) void l1_loss_bwd8_kernel(int B, int C, int H, int W, int bi,
+                                                           const float* __restrict__ pred, const float* __restrict__ gt,
+                                                           float inv_count, dbsr_tensor dpre,
+                                                           float* __restrict__ partial) {
+    const long long total = (long long)B * H * W;
+    const long long hw = (long long)H * W;
+    float s = 0.f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const long long idx = ((long long)blockIdx.x * 4 + u) * 256 + threadIdx.x;
+        if (idx >= total) break;
+        const int b = (int)(idx / hw);
+        const int rr = (int)(idx - (long long)b * hw);
+        const int y = rr / W, x = rr - y * W;
+        const bool in = y >= bi && y < H - bi && x >= bi && x < W - bi;
+        float gv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        for (int c = 0; c < C; ++c) {
+            const long long off = ((long long)b * C + c) * hw + rr;
+            const float pv = pred[off], d = pv - gt[off];
+            if (in) {
+                s += fabsf(d);
+                gv[c] = pv > 0.f ? (d > 0.f ? inv_count : (d < 0.f ? -inv_count : 0.f)) : 0.f;
+            }
+        }
+        store8(img_ptr<T>(dpre, b) + (long long)rr * 8, gv);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    __shared__ float red[4];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) partial[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
 // The predictor ReLU's backward from an arbitrary upstream gradient (autograd through DBSRNet.forward, any
 // objective): dpre[b][y][x][c] = [pred > 0] * gout[b][c][y][x] (fp32 NCHW in, NHWC out in the compute dtype).
 template <typename T>
@@ -311,6 +471,34 @@ __global__ __launch_bounds__(256) void unshuffle_gate_kernel(int B, int H, int W
     const float g = elem<T>::ld(img_ptr<T>(gate, b) + hr * gate.ld + c);
     const float v = g > 0.f ? elem<T>::ld(img_ptr<T>(ds, b) + hr * ds.ld + c) : 0.f;
     elem<T>::st(img_ptr<T>(du, b) + (long long)rr * du.ld + k, v);
+}
+
+// 16-B version: a block per low-res pixel (looping), thread = (sub-pixel, 8-channel group): 16-B loads of dS
+// and the gate, the block's K = C*s*s outputs transposed through the LDS into 16-B stores
+template <typename T>
+__global__ __launch_bounds__(256) void unshuffle_gate16_kernel(int B, int H, int W, int s, int C, dbsr_tensor ds,
+                                                               dbsr_tensor gate, dbsr_tensor du) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char ush[];
+    T* tile = (T*)ush;
+    const int ss = s * s, K = C * ss, groups = C / 8, tasks = ss * groups;
+    const long long npix = (long long)B * H * W;
+    for (long long pix = blockIdx.x; pix < npix; pix += gridDim.x) {
+        const int b = (int)(pix / ((long long)H * W)), rr = (int)(pix - (long long)b * H * W);
+        const int y = rr / W, x = rr - y * W;
+        for (int t = threadIdx.x; t < tasks; t += 256) {
+            const int sub = t / groups, cg = t - sub * groups, i = sub / s, j = sub - i * s;
+            const long long hr = (long long)(y * s + i) * (W * s) + (x * s + j);
+            float d[8], g[8];
+            load8(img_ptr<T>(ds, b) + hr * ds.ld + cg * 8, d);
+            load8(img_ptr<T>(gate, b) + hr * gate.ld + cg * 8, g);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) elem<T>::st(tile + (cg * 8 + e) * ss + sub, g[e] > 0.f ? d[e] : 0.f);
+        }
+        __syncthreads();
+        T* o = img_ptr<T>(du, b) + (long long)rr * du.ld;
+        for (int q = threadIdx.x; q < K / 8; q += 256) *(u32x4_t*)(o + q * 8) = *(const u32x4_t*)(tile + q * 8);
+        __syncthreads();
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -430,6 +618,183 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(int n, int h, int w, int 
 }
 
 // ------------------------------------------------------------------------------------------------
+// warp backward as an owner-computes gather (no atomics on features, no fp32 scratch image).  The
+// contributions -- (output pixel p, bilinear weight) for each in-frame tap q of p -- are binned per
+// destination pixel q by a counting sort (wb_count: per-pixel counts; wb_scan: offsets per pair; wb_scatter:
+// 8-B records {p, weight}), then wb_gather runs one wave per destination pixel: lanes own 8 channels each
+// (16-B loads of dout[p]), the pixel's few contributions (4 on average) are summed in registers in record
+// order and the result is written once, gated by the encoder output's ReLU (encoders.py:66-72):
+// dfeat[q] = [gate[q] > 0] * sum_p w(p, q) dout[p].  Any flow field costs the same per contribution.  The
+// record order within a pixel follows the scatter's atomics, so fp32 sums are not bitwise reproducible.
+// ------------------------------------------------------------------------------------------------
+struct WarpTaps { int x0, y0; float wx1, wy1; };
+// bilinear taps of output pixel (x, y) (grid_sample, zeros, align_corners=False; as warp_kernel)
+__device__ __forceinline__ WarpTaps warp_taps(int x, int y, int w, int h, float fx, float fy) {
+    const float gx = ((float)x + 0.5f) + fx, gy = ((float)y + 0.5f) + fy;
+    const float gxn = 2.0f * gx / (float)w - 1.0f, gyn = 2.0f * gy / (float)h - 1.0f;
+    const float ix = ((gxn + 1.f) * (float)w - 1.f) / 2.f, iy = ((gyn + 1.f) * (float)h - 1.f) / 2.f;
+    const float fx0 = floorf(ix), fy0 = floorf(iy);
+    WarpTaps t;
+    // far-away / non-finite coordinates: no tap in the frame (x0 = -2 keeps both columns out)
+    const bool ok = fx0 >= -1.f && fx0 < (float)w && fy0 >= -1.f && fy0 < (float)h;
+    t.x0 = ok ? (int)fx0 : -2;
+    t.y0 = ok ? (int)fy0 : -2;
+    t.wx1 = ix - fx0;
+    t.wy1 = iy - fy0;
+    return t;
+}
+
+__global__ __launch_bounds__(256) void wb_count_kernel(int n, int h, int w, const float* __restrict__ flow,
+                                                       long long fis, int* __restrict__ counts) {
+    const int hw = h * w;
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long long)n * hw) return;
+    const int p = (int)(idx / hw), rr = (int)(idx - (long long)p * hw);
+    const float* fl = flow + (long long)p * fis;
+    const WarpTaps t = warp_taps(rr % w, rr / w, w, h, fl[rr], fl[hw + rr]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int xx = t.x0 + (k & 1), yy = t.y0 + (k >> 1);
+        if ((unsigned)xx < (unsigned)w && (unsigned)yy < (unsigned)h)
+            atomicAdd(&counts[(long long)p * hw + yy * w + xx], 1);
+    }
+}
+
+// per pair: exclusive prefix sum of the per-pixel counts -> offsets and scatter cursors.  One block per pair;
+// thread t scans 16 consecutive pixels serially, the block scans the 1024 thread totals, chunk by chunk.
+__global__ __launch_bounds__(1024) void wb_scan_kernel(int hw, const int* __restrict__ counts,
+                                                       int* __restrict__ offsets, int* __restrict__ cursor) {
+    constexpr int PER = 16;
+    const long long base_p = (long long)blockIdx.x * hw;
+    __shared__ int part[1024];
+    __shared__ int carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (int base = 0; base < hw; base += 1024 * PER) {
+        const int i0 = base + (int)threadIdx.x * PER;
+        int v[PER], tot = 0;
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            v[j] = i0 + j < hw ? counts[base_p + i0 + j] : 0;
+            tot += v[j];
+        }
+        part[threadIdx.x] = tot;
+        __syncthreads();
+        for (int o = 1; o < 1024; o <<= 1) {                // Hillis-Steele inclusive scan of the totals
+            const int a = (int)threadIdx.x >= o ? part[threadIdx.x - o] : 0;
+            __syncthreads();
+            part[threadIdx.x] += a;
+            __syncthreads();
+        }
+        int ex = carry + part[threadIdx.x] - tot;
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            if (i0 + j < hw) {
+                offsets[base_p + i0 + j] = ex;
+                cursor[base_p + i0 + j] = ex;
+            }
+            ex += v[j];
+        }
+        __syncthreads();
+        if (threadIdx.x == 1023) carry += part[1023];
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(256) void wb_scatter_kernel(int n, int h, int w, const float* __restrict__ flow,
+                                                         long long fis, int* __restrict__ cursor,
+                                                         int2* __restrict__ records) {
+    const int hw = h * w;
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long long)n * hw) return;
+    const int p = (int)(idx / hw), rr = (int)(idx - (long long)p * hw);
+    const float* fl = flow + (long long)p * fis;
+    const WarpTaps t = warp_taps(rr % w, rr / w, w, h, fl[rr], fl[hw + rr]);
+    int2* rec = records + (long long)p * 4 * hw;             // the pair's region: <= 4 records per pixel
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int xx = t.x0 + (k & 1), yy = t.y0 + (k >> 1);
+        if ((unsigned)xx >= (unsigned)w || (unsigned)yy >= (unsigned)h) continue;
+        const float wt = ((k & 1) ? t.wx1 : 1.f - t.wx1) * ((k >> 1) ? t.wy1 : 1.f - t.wy1);
+        const int pos = atomicAdd(&cursor[(long long)p * hw + yy * w + xx], 1);
+        rec[pos] = int2{rr, __float_as_int(wt)};
+    }
+}
+
+// one wave per destination pixel; lanes = 8-channel groups (16-B loads), channel passes of 512
+template <typename T>
+__global__ __launch_bounds__(256) void wb_gather_kernel(int n, int h, int w, int C, dbsr_tensor dout,
+                                                        const int* __restrict__ counts, const int* __restrict__ offsets,
+                                                        const int2* __restrict__ records, dbsr_tensor gate,
+                                                        dbsr_tensor dfeat) {
+    const int hw = h * w;
+    const int lane = threadIdx.x & 63;
+    const long long q = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= (long long)n * hw) return;
+    const int p = (int)(q / hw), rr = (int)(q - (long long)p * hw);
+    const int cnt = counts[q];
+    const int2* rec = records + (long long)p * 4 * hw + offsets[q];
+    const T* src = img_ptr<T>(dout, p);
+    T* dst = img_ptr<T>(dfeat, p) + (long long)rr * dfeat.ld;
+    const T* gp = gate.ptr ? img_ptr<T>(gate, p) + (long long)rr * gate.ld : nullptr;
+    for (int c0 = 0; c0 < C; c0 += 512) {
+        const int c = c0 + lane * 8;
+        if (c >= C) break;
+        float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        for (int e0 = 0; e0 < cnt; e0 += 4) {
+            float d[4][8];
+            float wt[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (e0 + u < cnt) {
+                    const int2 r = rec[e0 + u];
+                    wt[u] = __int_as_float(r.y);
+                    load8(src + (long long)r.x * dout.ld + c, d[u]);
+                } else {
+                    wt[u] = 0.f;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) d[u][j] = 0.f;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) a[j] = fmaf(wt[u], d[u][j], a[j]);
+        }
+        if (gp) {
+            float g[8];
+            load8(gp + c, g);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) a[j] = g[j] > 0.f ? a[j] : 0.f;
+        }
+        store8(dst + c, a);
+    }
+}
+
+__global__ void zero_ints_kernel(long long n, int* __restrict__ p) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = 0;
+}
+
+// out[f] = [gate[f] > 0] * in[f] over n images of c channels (8 per thread, 16-B accesses)
+template <typename T>
+__global__ __launch_bounds__(256) void gate_copy_kernel(int n, int hw, int c, dbsr_tensor in, dbsr_tensor gate,
+                                                        dbsr_tensor out) {
+    const int groups = c / 8;
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long long)n * hw * groups) return;
+    const int g = (int)(idx % groups);
+    const long long pix = idx / groups;
+    const int f = (int)(pix / hw), rr = (int)(pix - (long long)f * hw);
+    float d[8], e[8];
+    load8(img_ptr<T>(in, f) + (long long)rr * in.ld + g * 8, d);
+    load8(img_ptr<T>(gate, f) + (long long)rr * gate.ld + g * 8, e);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d[j] = e[j] > 0.f ? d[j] : 0.f;
+    store8(img_ptr<T>(out, f) + (long long)rr * out.ld + g * 8, d);
+}
+
+// ------------------------------------------------------------------------------------------------
 // Encoder output gradient assembly (encoders.py:66-80 + the out_layer ReLU): frame (b, n):
 //   n == 0: dE = dref[b];  n >= 1: dE = dsrc32[b*N+n] (the warp scatter)
 // times [E > 0], into dE (images b*N+n).
@@ -492,13 +857,16 @@ __global__ void dgrad_weights_kernel(const float* __restrict__ w, int cout, int 
 }  // namespace
 
 // ================================================================================================
+static int wgrad_cb(int cin, int cout) { return (cin <= 32 && cout <= 32) ? 32 : 64; }
+
 extern "C" size_t dbsr_conv_wgrad_workspace_bytes(int n_frames, int h, int w, int cin, int cout, int k) {
     if (n_frames <= 0 || h <= 0 || w <= 0 || cin <= 0 || cout <= 0 || (k != 1 && k != 3)) return 0;
+    const int cb = wgrad_cb(cin, cout);
     const long long units = (long long)n_frames * ((h + WG_TH - 1) / WG_TH) * ((w + WG_TW - 1) / WG_TW);
-    const int nty = (cout + 63) / 64, ntz = (cin + 63) / 64;
-    const long long nbx = std::max<long long>(1, std::min<long long>(units, std::max(1, 1024 / (nty * ntz))));
+    const int nty = (cout + cb - 1) / cb, ntz = (cin + cb - 1) / cb;
+    const long long nbx = std::max<long long>(1, std::min<long long>(units, std::max(1, wg_blocks(cb) / (nty * ntz))));
     const int nw = k == 3 ? 9 : 4;
-    return (size_t)nbx * nty * ntz * nw * 64 * 64 * sizeof(float);
+    return (size_t)nbx * nty * ntz * nw * cb * cb * sizeof(float);
 }
 
 extern "C" int dbsr_conv_wgrad(int n_frames, int h, int w, dbsr_tensor x, int cin, dbsr_tensor dy, int cout, int k,
@@ -514,8 +882,9 @@ extern "C" int dbsr_conv_wgrad(int n_frames, int h, int w, dbsr_tensor x, int ci
     const size_t need = dbsr_conv_wgrad_workspace_bytes(n_frames, h, w, cin, cout, k);
     DBSR_CHECK_ARG(workspace_bytes >= need, "conv_wgrad: workspace %zu < %zu bytes", workspace_bytes, need);
     const long long units = (long long)n_frames * ((h + WG_TH - 1) / WG_TH) * ((w + WG_TW - 1) / WG_TW);
-    const int nty = (cout + 63) / 64, ntz = (cin + 63) / 64;
-    const int nbx = (int)std::max<long long>(1, std::min<long long>(units, std::max(1, 1024 / (nty * ntz))));
+    const int cb = wgrad_cb(cin, cout);
+    const int nty = (cout + cb - 1) / cb, ntz = (cin + cb - 1) / cb;
+    const int nbx = (int)std::max<long long>(1, std::min<long long>(units, std::max(1, wg_blocks(cb) / (nty * ntz))));
     const int nw = k == 3 ? 9 : 4;
     float* part = (float*)workspace;
     hipStream_t s = (hipStream_t)stream;
@@ -528,26 +897,27 @@ extern "C" int dbsr_conv_wgrad(int n_frames, int h, int w, dbsr_tensor x, int ci
     const dim3 grid(nbx, nty, ntz);
     int rc = by_dtype(x.dtype, [&](auto* tag) {
         using T = std::remove_pointer_t<decltype(tag)>;
-        if (k == 3)
-            hipLaunchKernelGGL((conv_wgrad_kernel<T, 3>), grid, dim3(576), 0, s, n_frames, h, w, xx, cin, dd, cout,
-                               units, part);
-        else
-            hipLaunchKernelGGL((conv_wgrad_kernel<T, 1>), grid, dim3(256), 0, s, n_frames, h, w, xx, cin, dd, cout,
-                               units, part);
+#define DBSR_WG(KK, CBB) hipLaunchKernelGGL((conv_wgrad_kernel<T, KK, CBB>), grid, dim3(KK == 3 ? 576 : 256), 0, s, \
+                                           n_frames, h, w, xx, cin, dd, cout, units, part)
+        if (k == 3) {
+            if (cb == 32) DBSR_WG(3, 32); else DBSR_WG(3, 64);
+        } else {
+            if (cb == 32) DBSR_WG(1, 32); else DBSR_WG(1, 64);
+        }
+#undef DBSR_WG
         DBSR_LAUNCH_CHECK();
         return 0;
     });
     if (rc) return rc;
-    const long long total = (long long)cout * cin * k * k;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(nblocks(total, 256)), dim3(256), 0, s, nbx, nty, ntz, nw, k * k, cout,
-                       cin, part, dw, accumulate);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)(cout * k * k * ((cin + 63) / 64))), dim3(256), 0, s, nbx,
+                       nty, ntz, nw, k * k, cout, cin, cb, part, dw, accumulate);
     DBSR_LAUNCH_CHECK();
     return 0;
 }
 
 extern "C" size_t dbsr_chan_sum_workspace_bytes(int n, int hw, int c) {
     const long long total = (long long)n * hw;
-    const long long nbx = std::min<long long>(512, std::max<long long>(1, (total + 255) / 256));
+    const long long nbx = std::min<long long>(1024, std::max<long long>(1, (total + 255) / 256));
     return (size_t)nbx * c * sizeof(float);
 }
 
@@ -556,19 +926,34 @@ extern "C" int dbsr_chan_sum(int n, int hw, int c, dbsr_tensor t, float* out, in
     DBSR_CHECK_ARG(map_ok(t) && out && workspace && n > 0 && hw > 0 && c > 0, "chan_sum: bad arguments");
     DBSR_CHECK_ARG(workspace_bytes >= dbsr_chan_sum_workspace_bytes(n, hw, c), "chan_sum: workspace too small");
     const long long total = (long long)n * hw;
-    const int nbx = (int)std::min<long long>(512, std::max<long long>(1, (total + 255) / 256));
+    const int nbx = (int)std::min<long long>(1024, std::max<long long>(1, (total + 255) / 256));
     const int ppb = (int)((total + nbx - 1) / nbx);
     hipStream_t s = (hipStream_t)stream;
+    const int groups = (c + 7) / 8;
+    int tpp = 1;
+    while (tpp < groups) tpp *= 2;
+    // 16-B loads need 8-element-aligned pixels and channel slices; channels c .. groups*8 of a pixel are read
+    // and summed into LDS columns that the final reduction never reads
+    const bool v16 = t.dtype != DBSR_F32 && vec_ok(t, 8) && t.ld >= t.c0 + groups * 8 && tpp <= 64;
     int rc = by_dtype(t.dtype, [&](auto* tag) {
         using T = std::remove_pointer_t<decltype(tag)>;
+        if constexpr (sizeof(T) == 2) {
+            if (v16) {
+#define DBSR_CS16(P) if (tpp == P) hipLaunchKernelGGL((chan_sum16_kernel<T, P>), dim3(nbx), dim3(256), 0, s, n, hw, c, t, ppb, (float*)workspace);
+                DBSR_CS16(1) DBSR_CS16(2) DBSR_CS16(4) DBSR_CS16(8) DBSR_CS16(16) DBSR_CS16(32) DBSR_CS16(64)
+#undef DBSR_CS16
+                DBSR_LAUNCH_CHECK();
+                return 0;
+            }
+        }
         hipLaunchKernelGGL((chan_sum_kernel<T>), dim3(nbx, (c + 63) / 64), dim3(256), 0, s, n, hw, c, t, ppb,
                            (float*)workspace);
         DBSR_LAUNCH_CHECK();
         return 0;
     });
     if (rc) return rc;
-    hipLaunchKernelGGL(sum_rows_kernel, dim3(nblocks(c, 256)), dim3(256), 0, s, nbx, c, (const float*)workspace, out,
-                       accumulate, 1.0f);
+    hipLaunchKernelGGL(sum_rows_kernel, dim3((unsigned)((c + 63) / 64)), dim3(256), 0, s, nbx, c,
+                       (const float*)workspace, out, accumulate, 1.0f);
     DBSR_LAUNCH_CHECK();
     return 0;
 }
@@ -584,15 +969,25 @@ extern "C" int dbsr_l1_loss_backward(int B, int C, int H, int W, int boundary_ig
     DBSR_CHECK_ARG(workspace_bytes >= nb * sizeof(float), "l1_loss_backward: workspace < %u floats", nb);
     const float count = (float)B * C * (H - 2 * boundary_ignore) * (W - 2 * boundary_ignore);
     hipStream_t s = (hipStream_t)stream;
+    const bool v8 = dpre.dtype != DBSR_F32 && dpre.ld == 8 && dpre.c0 == 0 && C <= 8;
+    const unsigned nb8 = nblocks(total, 1024);            // 4 pixels per thread
     int rc = by_dtype(dpre.dtype, [&](auto* tag) {
         using T = std::remove_pointer_t<decltype(tag)>;
+        if constexpr (sizeof(T) == 2) {
+            if (v8) {
+                hipLaunchKernelGGL((l1_loss_bwd8_kernel<T>), dim3(nb8), dim3(256), 0, s, B, C, H, W, boundary_ignore,
+                                   pred, gt, 1.0f / count, dpre, (float*)workspace);
+                DBSR_LAUNCH_CHECK();
+                return 0;
+            }
+        }
         hipLaunchKernelGGL((l1_loss_bwd_kernel<T>), dim3(nb), dim3(256), 0, s, B, C, H, W, boundary_ignore, pred, gt,
                            1.0f / count, dpre, (float*)workspace);
         DBSR_LAUNCH_CHECK();
         return 0;
     });
     if (rc) return rc;
-    hipLaunchKernelGGL(sum_rows_kernel, dim3(1), dim3(256), 0, s, (int)nb, 1, (const float*)workspace, loss, 0,
+    hipLaunchKernelGGL(sum_all_kernel, dim3(1), dim3(256), 0, s, (int)(v8 ? nb8 : nb), (const float*)workspace, loss,
                        1.0f / count);
     DBSR_LAUNCH_CHECK();
     return 0;
@@ -617,8 +1012,20 @@ extern "C" int dbsr_unshuffle_gate(int B, int H, int W, int s, int c, dbsr_tenso
                    "unshuffle_gate: bad tensors");
     DBSR_CHECK_ARG(B > 0 && H > 0 && W > 0 && s > 0 && c > 0 && du.ld >= du.c0 + c * s * s, "unshuffle_gate: sizes");
     const long long total = (long long)B * H * W * c * s * s;
+    const int K = c * s * s;
+    const bool v16 = ds.dtype != DBSR_F32 && c % 8 == 0 && vec_ok(ds, 8) && vec_ok(gate, 8) && vec_ok(du, 8) &&
+                     K % 8 == 0 && K * 2 <= 32768;
     return by_dtype(ds.dtype, [&](auto* tag) {
         using T = std::remove_pointer_t<decltype(tag)>;
+        if constexpr (sizeof(T) == 2) {
+            if (v16) {
+                const long long npix = (long long)B * H * W;
+                hipLaunchKernelGGL((unshuffle_gate16_kernel<T>), dim3((unsigned)std::min<long long>(npix, 65536)),
+                                   dim3(256), K * 2, (hipStream_t)stream, B, H, W, s, c, ds, gate, du);
+                DBSR_LAUNCH_CHECK();
+                return 0;
+            }
+        }
         hipLaunchKernelGGL((unshuffle_gate_kernel<T>), dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, B,
                            H, W, s, c, ds, gate, du);
         DBSR_LAUNCH_CHECK();
@@ -685,6 +1092,60 @@ extern "C" int dbsr_enc_grad_gate(int B, int N, int hw, int c, dbsr_tensor dref,
         using T = std::remove_pointer_t<decltype(tag)>;
         hipLaunchKernelGGL((enc_grad_gate_kernel<T>), dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, B,
                            N, hw, c, dref, dsrc32, e, de);
+        DBSR_LAUNCH_CHECK();
+        return 0;
+    });
+}
+
+extern "C" size_t dbsr_warp_backward_gather_workspace_bytes(int n, int h, int w) {
+    if (n <= 0 || h <= 0 || w <= 0) return 0;
+    const long long px = (long long)n * h * w;
+    return (size_t)(3 * px * sizeof(int) + 15) / 16 * 16 + (size_t)px * 4 * sizeof(int2);
+}
+
+extern "C" int dbsr_warp_backward_gather(int n, int h, int w, int c, dbsr_tensor dout, const float* flow,
+                                         long long flow_img_stride, dbsr_tensor gate, dbsr_tensor dfeat,
+                                         void* workspace, size_t workspace_bytes, void* stream) {
+    DBSR_CHECK_ARG(map_ok(dout) && map_ok(dfeat) && flow && workspace && dout.dtype == dfeat.dtype,
+                   "warp_backward_gather: bad tensors");
+    DBSR_CHECK_ARG(!gate.ptr || (map_ok(gate) && gate.dtype == dfeat.dtype), "warp_backward_gather: bad gate");
+    DBSR_CHECK_ARG(n > 0 && h > 0 && w > 0 && c > 0 && c % 8 == 0 && vec_ok(dout, 8) && vec_ok(dfeat, 8) &&
+                   (!gate.ptr || vec_ok(gate, 8)) && (long long)h * w * 4 < (1LL << 31),
+                   "warp_backward_gather: c, ld and c0 must be multiples of 8");
+    DBSR_CHECK_ARG(workspace_bytes >= dbsr_warp_backward_gather_workspace_bytes(n, h, w),
+                   "warp_backward_gather: workspace %zu < %zu bytes", workspace_bytes,
+                   dbsr_warp_backward_gather_workspace_bytes(n, h, w));
+    const long long px = (long long)n * h * w;
+    int* counts = (int*)workspace;
+    int* offsets = counts + px;
+    int* cursor = offsets + px;
+    int2* records = (int2*)((char*)workspace + (3 * px * sizeof(int) + 15) / 16 * 16);
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(zero_ints_kernel, dim3(nblocks(px, 256)), dim3(256), 0, s, px, counts);
+    hipLaunchKernelGGL(wb_count_kernel, dim3(nblocks(px, 256)), dim3(256), 0, s, n, h, w, flow, flow_img_stride, counts);
+    hipLaunchKernelGGL(wb_scan_kernel, dim3(n), dim3(1024), 0, s, h * w, counts, offsets, cursor);
+    hipLaunchKernelGGL(wb_scatter_kernel, dim3(nblocks(px, 256)), dim3(256), 0, s, n, h, w, flow, flow_img_stride,
+                       cursor, records);
+    DBSR_LAUNCH_CHECK();
+    return by_dtype(dout.dtype, [&](auto* tag) {
+        using T = std::remove_pointer_t<decltype(tag)>;
+        hipLaunchKernelGGL((wb_gather_kernel<T>), dim3(nblocks(px, 4)), dim3(256), 0, s, n, h, w, c, dout, counts,
+                           offsets, records, gate, dfeat);
+        DBSR_LAUNCH_CHECK();
+        return 0;
+    });
+}
+
+extern "C" int dbsr_gate_copy(int n, int hw, int c, dbsr_tensor in, dbsr_tensor gate, dbsr_tensor out, void* stream) {
+    DBSR_CHECK_ARG(map_ok(in) && map_ok(gate) && map_ok(out) && in.dtype == gate.dtype && out.dtype == in.dtype,
+                   "gate_copy: bad tensors");
+    DBSR_CHECK_ARG(n > 0 && hw > 0 && c % 8 == 0 && vec_ok(in, 8) && vec_ok(gate, 8) && vec_ok(out, 8),
+                   "gate_copy: layout");
+    const long long total = (long long)n * hw * (c / 8);
+    return by_dtype(in.dtype, [&](auto* tag) {
+        using T = std::remove_pointer_t<decltype(tag)>;
+        hipLaunchKernelGGL((gate_copy_kernel<T>), dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, n, hw,
+                           c, in, gate, out);
         DBSR_LAUNCH_CHECK();
         return 0;
     });

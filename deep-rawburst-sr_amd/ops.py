@@ -267,3 +267,38 @@ def warp_backward(dout, flow):
                                        L.FrameMap(1, 1, 0, 1), H * W * C, L.stream_ptr(dout.device)),
             'dbsr_warp_backward')
     return out.permute(0, 3, 1, 2).contiguous()
+
+
+def warp_backward_gather(dout, flow, gate=None):
+    """dL/dfeat of warp(feat, flow) (warp.py:19-46) by the owner-computes gather kernel, optionally times
+    [gate > 0] (the encoder's ReLU): dout [N,C,H,W] (fp32 / bf16 / fp16), flow [N,2,H,W], gate like dout ->
+    [N,C,H,W] in dout's dtype."""
+    _need_cuda(dout, flow)
+    N, C, H, W = dout.shape
+    dev = dout.device
+    d = dout.permute(0, 2, 3, 1).contiguous()
+    fl = flow.to(torch.float32).contiguous()
+    out = torch.empty_like(d)
+    g = gate.to(dout.dtype).permute(0, 2, 3, 1).contiguous() if gate is not None else None
+    need = L.lib().dbsr_warp_backward_gather_workspace_bytes(N, H, W)
+    ws = torch.empty(need, dtype=torch.uint8, device=dev)
+    L.check(L.lib().dbsr_warp_backward_gather(N, H, W, C, L.tensor_desc(d, C), fl.data_ptr(), 2 * H * W,
+                                              L.tensor_desc(g, C) if g is not None else L.NULL_TENSOR,
+                                              L.tensor_desc(out, C), ws.data_ptr(), need, L.stream_ptr(dev)),
+            'dbsr_warp_backward_gather')
+    return out.permute(0, 3, 1, 2).contiguous()
+
+
+def chan_sum(t):
+    """Per-channel sum over batch and pixels (the conv bias gradient) of t [N,C,H,W] -> fp32 [C]."""
+    _need_cuda(t)
+    N, C, H, W = t.shape
+    ld = (C + 7) // 8 * 8
+    x = torch.zeros(N, H, W, ld, dtype=t.dtype, device=t.device)
+    x[..., :C] = t.permute(0, 2, 3, 1)
+    out = torch.empty(C, dtype=torch.float32, device=t.device)
+    need = L.lib().dbsr_chan_sum_workspace_bytes(N, H * W, C)
+    ws = torch.empty(max(need // 4, 1), dtype=torch.float32, device=t.device)
+    L.check(L.lib().dbsr_chan_sum(N, H * W, C, L.tensor_desc(x, ld), out.data_ptr(), 0, ws.data_ptr(), need,
+                                  L.stream_ptr(t.device)), 'dbsr_chan_sum')
+    return out

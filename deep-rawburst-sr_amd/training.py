@@ -402,14 +402,16 @@ class DBSRTrainer:
         dEref = NHWC(B, H, W, C, dt, dev)
         plan.conv('bwd.proj.ref', self.proj.bwd, B, dPJ, 0, hw, dEref, 0, L.ACT_NONE, xmap=(1, N, 0, 1), res=dF0)
         dWf = NHWC(max(P, 1), H, W, C, dt, dev)
-        dE32 = torch.zeros(F, H, W, C, dtype=torch.float32, device=dev)
-        plan.add('zero.dE32', lib.dbsr_zero, dE32.data_ptr(), dE32.numel() * 4)
+        dE = NHWC(F, H, W, C, dt, dev)
         if P > 0:
             plan.conv('bwd.proj.oth', self.proj.bwd, P, dPJ, 0, hw, dWf, 0, L.ACT_NONE, xmap=(N - 1, N, 1, 1), res=dWfF)
-            plan.add('bwd.warp', lib.dbsr_warp_backward, P, H, W, C, dWf.d(0), offsets.data_ptr(), 2 * H * W,
-                     dE32.data_ptr(), L.FrameMap(N - 1, N, 1, 1), H * W * C)
-        dE = NHWC(F, H, W, C, dt, dev)
-        plan.add('bwd.enc.gate', lib.dbsr_enc_grad_gate, B, N, H * W, C, dEref.d(0), dE32.data_ptr(), E.d(0), dE.d(0))
+            # warp backward (owner-computes gather, no atomics) straight into the other frames' encoder-output
+            # gradient, gated by the encoder's output ReLU (encoders.py:66-80)
+            need = lib.dbsr_warp_backward_gather_workspace_bytes(P, H, W)
+            plan.add('bwd.warp', lib.dbsr_warp_backward_gather, P, H, W, C, dWf.d(0), offsets.data_ptr(), 2 * H * W,
+                     E.d(0, (N - 1, N, 1, 1)), dE.d(0, (N - 1, N, 1, 1)), ws('wb', need), need)
+        plan.add('bwd.enc.gate', lib.dbsr_gate_copy, B, H * W, C, dEref.d(0), E.d(0, (1, N, 0, 1)),
+                 dE.d(0, (1, N, 0, 1)))
         # encoder
         wgrad('enc.out', self.enc_out, F, H, W, e_last, 0, dE, 0)
         bgrad('enc.out', self.enc_out, F, H * W, dE, 0)
@@ -430,7 +432,7 @@ class DBSRTrainer:
                                lane)
         plan.finalize_workspace(dev)
         plan.keep.extend([raw, rgb, om, flow_out, WP, o0, e0, E, PJ, Wf, q0, LG, FUS, FW, g0, S0, S1, dP, gh, dS0, dU,
-                          gp, dFUS, dLG, dF0, dWfF, gq, dWP, dPJ, dEref, dWf, dE32, dE, ge, ofe_s, enc_s, wp_s, pre_s,
+                          gp, dFUS, dLG, dF0, dWfF, gq, dWP, dPJ, dEref, dWf, dE, ge, ofe_s, enc_s, wp_s, pre_s,
                           post_s, scratch])
         plan.bufs = bufs
         plan.buckets = buckets

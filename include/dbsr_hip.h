@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define DBSR_ABI_VERSION 11
+#define DBSR_ABI_VERSION 12
 
 enum { DBSR_F32 = 0, DBSR_BF16 = 1, DBSR_F16 = 2 };
 enum { DBSR_ACT_NONE = 0, DBSR_ACT_RELU = 1, DBSR_ACT_LRELU = 2 };      /* LeakyReLU slope 0.1 */
@@ -314,6 +314,17 @@ int dbsr_warp_backward(int n, int h, int w, int c, dbsr_tensor dout, const float
 /* encoder output gradient (encoders.py:66-80): de[b*N+n] = [e > 0] * (n == 0 ? dref[b] : dsrc32[b*N+n]). */
 int dbsr_enc_grad_gate(int B, int N, int hw, int c, dbsr_tensor dref, const float* dsrc32, dbsr_tensor e,
                        dbsr_tensor de, void* stream);
+/* warp backward w.r.t. the features (warp.py:19-46) as an owner-computes gather, replacing the atomics of
+ * dbsr_warp_backward: dfeat[p] = [gate[p] > 0] * (bilinear-transpose of dout[p]) (gate.ptr NULL: no gate),
+ * written whole (no accumulation, no fp32 scratch); c channels (c, ld, c0 multiples of 8), dout / gate / dfeat
+ * of one dtype.  The contributions are binned per destination pixel by a counting sort in `workspace` (any
+ * flow field); each pixel's fp32 sum runs in record order, which follows the binning's atomics. */
+size_t dbsr_warp_backward_gather_workspace_bytes(int n, int h, int w);
+int dbsr_warp_backward_gather(int n, int h, int w, int c, dbsr_tensor dout, const float* flow,
+                              long long flow_img_stride, dbsr_tensor gate, dbsr_tensor dfeat, void* workspace,
+                              size_t workspace_bytes, void* stream);
+/* out = [gate > 0] * in over n NHWC images of c channels (c, ld, c0 multiples of 8). */
+int dbsr_gate_copy(int n, int hw, int c, dbsr_tensor in, dbsr_tensor gate, dbsr_tensor out, void* stream);
 /* torch.optim.Adam step (weight_decay 0) on flat fp32 buffers; grad is scaled by grad_scale first. */
 int dbsr_adam_step(long long n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq, float lr,
                    float beta1, float beta2, float eps, int step, float grad_scale, void* stream);

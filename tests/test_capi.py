@@ -63,7 +63,8 @@ def test_splitk_workspace_query(L):
 
 def test_pointwise_dispatch(L):
     """dbsr_conv_kernel_for (host logic only): the merge's 1x1 512->64 projection over 104 frames takes the
-    pointwise kernel (5); fp32, a residual, a non-power-of-two cin or a tiny pixel count do not."""
+    pointwise kernel (5), and so does the training dgrad of it (64 -> 512 + residual); fp32, a gate, a
+    misaligned residual, a non-power-of-two cin or a tiny pixel count do not."""
     lib = L.lib()
     d = L.ConvDesc()
     d.n_frames = 104
@@ -84,8 +85,17 @@ def test_pointwise_dispatch(L):
     assert lib.dbsr_conv_kernel_for(d) != 5
     d.n_frames, d.in_h, d.in_w, d.out_h, d.out_w = 104, 48, 48, 48, 48
     d.res = L.Tensor(1, L.DBSR_BF16, 48 * 48 * 32, 32, 0, L.FrameMap(1, 1, 0, 1))
+    assert lib.dbsr_conv_kernel_for(d) == 5
+    d.res = L.Tensor(1, L.DBSR_BF16, 48 * 48 * 36, 36, 0, L.FrameMap(1, 1, 0, 1))   # ld not 16-B aligned
     assert lib.dbsr_conv_kernel_for(d) != 5
     d.res = L.NULL_TENSOR
+    d.gate = L.Tensor(1, L.DBSR_BF16, 48 * 48 * 32, 32, 0, L.FrameMap(1, 1, 0, 1))
+    assert lib.dbsr_conv_kernel_for(d) != 5
+    d.gate = L.NULL_TENSOR
+    d.cin, d.cout = 64, 512                                                   # dgrad of the projection
+    d.y = L.Tensor(1, L.DBSR_BF16, 48 * 48 * 512, 512, 0, L.FrameMap(1, 1, 0, 1))
+    assert lib.dbsr_conv_kernel_for(d) == 5
+    d.cin, d.cout = 512, 32
     d.x.dtype = d.y.dtype = L.DBSR_F32
     assert lib.dbsr_conv_kernel_for(d) != 5
 

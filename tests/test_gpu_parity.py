@@ -164,7 +164,12 @@ PIPE16 = [(2, False, 0, 117, 128, 16), (2, False, 0, 565, 128, 16), (2, False, 0
           (2, False, 0, 469, 64, 16)]
 
 
-@pytest.mark.parametrize('case', PIPE_EPI + PIPE16)
+# the 32x16 tile (frame widths that are multiples of 32 but not 48: the training step's 128x128 frames)
+PIPE32 = [(1, False, 0, 128, 128, 32), (0, True, 1, 128, 128, 64), (0, False, 0, 128, 512, 64),
+          (1, False, 0, 192, 128, 64)]
+
+
+@pytest.mark.parametrize('case', PIPE_EPI + PIPE16 + PIPE32)
 def test_pipe_epilogue_variants(ops_mod, case):
     from dbsr_amd import _lib
     act, use_res, post, cin, cout = case[:5]

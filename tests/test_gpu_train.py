@@ -31,8 +31,10 @@ def _rel(a, b):
 
 @pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize('case', [(2, 64, 20, 36, 64, 3), (1, 4, 9, 17, 64, 3), (2, 512, 8, 16, 64, 1),
-                                  (1, 32, 24, 40, 3, 1), (1, 128, 12, 12, 512, 3), (2, 192, 16, 16, 128, 3)])
+                                  (1, 32, 24, 40, 3, 1), (1, 128, 12, 12, 512, 3), (2, 192, 16, 16, 128, 3),
+                                  (3, 32, 20, 36, 32, 3), (1, 32, 33, 47, 3, 3), (2, 24, 16, 40, 32, 1)])
 def test_conv_wgrad(ops, dtype, case):
+    # (the last three run the 32-channel-block variant with two tiles prefetched)
     N, Cin, H, W, Cout, k = case
     gen = torch.Generator().manual_seed(Cin + Cout * 3 + H)
     x = torch.randn(N, Cin, H, W, generator=gen)
@@ -92,6 +94,38 @@ def test_warp_backward(ops):
     orc.warp(x, fl).backward(dy)
     out = ops.warp_backward(dy.to(DEV), fl.to(DEV)).cpu()
     assert _rel(out, x.grad) <= 1e-5
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('case', [(2, 3, 40, 56), (3, 32, 64, 64), (2, 64, 17, 23), (1, 512, 12, 20), (1, 72, 9, 9)])
+def test_chan_sum(ops, dtype, case):
+    """Bias gradient (per-channel sum): the 16-B kernel (16-bit, any c) and the element kernel (fp32)."""
+    N, C, H, W = case
+    t = torch.randn(N, C, H, W, generator=torch.Generator().manual_seed(C + H)).to(dtype)
+    out = ops.chan_sum(t.to(DEV)).cpu()
+    ref = t.double().sum(dim=(0, 2, 3))
+    assert float((out.double() - ref).abs().max()) <= 1e-4 * float(t.double().abs().sum(dim=(0, 2, 3)).max())
+
+
+@pytest.mark.parametrize('case', [(3, 16, 12, 20, 3.0, torch.float32, False),     # random flow: list flushes
+                                  (2, 64, 40, 56, 20.0, torch.float32, True),     # far taps, window = frame
+                                  (2, 72, 33, 47, 0.7, torch.float32, True),      # ragged tiles, C % 64 != 0
+                                  (2, 64, 32, 48, 2.0, torch.bfloat16, True)])
+def test_warp_backward_gather(ops, case):
+    """The owner-computes gather (no atomics) against autograd through the oracle's grid_sample warp,
+    with the encoder-ReLU gate of the training step."""
+    from oracle import dbsr_oracle as orc
+    N, C, H, W, scale, dtype, gated = case
+    gen = torch.Generator().manual_seed(C + H)
+    x = torch.randn(N, C, H, W, generator=gen, requires_grad=True)
+    fl = torch.randn(N, 2, H, W, generator=gen) * scale
+    dy = torch.randn(N, C, H, W, generator=gen).to(dtype).float()
+    gate = F.relu(torch.randn(N, C, H, W, generator=gen)).to(dtype) if gated else None
+    orc.warp(x, fl).backward(dy)
+    ref = x.grad * (gate.float() > 0) if gated else x.grad
+    out = ops.warp_backward_gather(dy.to(DEV).to(dtype), fl.to(DEV), gate.to(DEV) if gated else None).float().cpu()
+    tol = 1e-5 if dtype == torch.float32 else 8e-3
+    assert _rel(out, ref) <= tol
 
 
 # ----------------------------------------------------------------------------------------------------
