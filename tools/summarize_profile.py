@@ -25,7 +25,7 @@ KERNELS = {   # label -> (name predicate, algorithmic bytes per launch at the de
 # kernel name -> bench.py family (bench.py CONV_FAMILIES / roofline_hbm keys)
 FAMILY = [('conv3x3_ws_kernel', 'conv3x3_ws'), ('conv3x3_pipe_kernel', 'conv3x3_pipe'),
           ('conv3x3_tiled_kernel', 'conv3x3_tiled'), ('conv1x1_kernel', 'conv1x1'),
-          ('upsample_shuffle_kernel', 'conv1x1_shuffle'), ('pwc_dense_kernel', 'pwc_dense'),
+          ('upsample_shuffle_kernel', 'conv1x1_shuffle'), ('pwc_dense', 'pwc_dense'),
           ('pwc_extract_kernel', 'pwc_extract'), ('warp512_bf16_kernel', 'warp'), ('fuse512_bf16_kernel', 'fuse')]
 
 
@@ -62,7 +62,7 @@ def main():
     shutil.copy(os.path.join(src, 'trace', 'run_kernel_stats.csv'), os.path.join(outdir, f'{tag}_kernel_stats.csv'))
     lines = [f'# rocprofv3 summary {tag}', '',
              'Command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline`',
-             '(bf16, batch 8 x 14 frames x 48x48; includes bench.py\'s per-op timing pass, so call counts are not',
+             '(fp16, batch 8 x 14 frames x 48x48; includes bench.py\'s per-op timing pass, so call counts are not',
              'one forward). Full CSV: `%s_kernel_stats.csv`.' % tag, '',
              '| kernel | calls | total ms | avg us | % |', '|---|---|---|---|---|']
     for r in stats[:25]:
@@ -94,6 +94,18 @@ def main():
         lines.append('| %s | %d | %.1f | %.1f | %.1f |' % (fam, t['dispatches'], t['fetch_bytes'] / 1e6,
                                                           t['write_bytes'] / 1e6, t['bytes_per_launch'] / 1e6))
     json.dump(traffic, open(os.path.join(outdir, 'pmc_traffic.json'), 'w'), indent=1)
+    tstats = os.path.join(src, 'train', 'run_kernel_stats.csv')
+    if os.path.exists(tstats):
+        shutil.copy(tstats, os.path.join(outdir, f'{tag}_train_kernel_stats.csv'))
+        rows = list(csv.DictReader(open(tstats)))
+        lines += ['', '## Training leg: `rocprofv3 --kernel-trace --stats -- python3 bench.py --mode train --steps 3 '
+                  '--warmup 1`', '(bf16, 8 x 14 x 128x128; includes the per-op timing pass). Full CSV: '
+                  '`%s_train_kernel_stats.csv`.' % tag, '',
+                  '| kernel | calls | total ms | avg us | % |', '|---|---|---|---|---|']
+        for r in rows[:25]:
+            lines.append('| `%s` | %s | %.2f | %.1f | %s |' % (r['Name'][:110], r['Calls'],
+                                                            float(r['TotalDurationNs']) / 1e6,
+                                                            float(r['AverageNs']) / 1e3, r['Percentage']))
     open(os.path.join(outdir, f'{tag}_summary.md'), 'w').write('\n'.join(lines) + '\n')
     print('\n'.join(lines))
 
