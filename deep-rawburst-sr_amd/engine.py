@@ -200,10 +200,24 @@ class Plan:
         if not Plan.MULTI_STREAM:
             return
         if lane not in self.streams:
-            self.streams[lane] = torch.cuda.Stream(device=device, priority=priority)
+            self.streams[lane] = Plan.side_stream(device, lane, priority)
         self.lanes.add(lane)
         self.ops.append((Plan.FORK, (torch.cuda.Event(),), f'sync.fork{lane}', lane))
         self.lane = lane
+
+    _side_streams = {}
+
+    @staticmethod
+    def side_stream(device, lane, priority):
+        """One side stream per (device, lane, priority) for the whole process, shared by every plan (the plans
+        of a process are ordered on the caller's stream anyway; a stream per plan only multiplied the HIP
+        streams, and hence the hardware-queue sharing, of a process)."""
+        dev = torch.device(device)
+        key = (dev.index if dev.index is not None else torch.cuda.current_device(), lane, priority)
+        st = Plan._side_streams.get(key)
+        if st is None:
+            st = Plan._side_streams[key] = torch.cuda.Stream(device=device, priority=priority)
+        return st
 
     def switch(self, lane):
         """Following ops go to `lane` (an already forked side lane, or 0), with no ordering edge."""
@@ -787,7 +801,7 @@ class DBSREngine:
         # lane-0 persistent convs issued while the side lane runs leave part of the CUs to it
         plan_cap = int(torch.cuda.get_device_properties(dev).multi_processor_count * DBSREngine.LANE0_CU_SHARE) \
             if Plan.MULTI_STREAM else 0
-        plan.fork(1, dev, priority=-1)
+        plan.fork(1, dev, priority=0)
         WP = self._emit_flow(plan, grp, N, H, W, sh)          # PWC-Net on lane 1
         plan.switch(0)
         plan.max_blocks = plan.max_blocks_cap = plan_cap
@@ -885,7 +899,12 @@ class DBSREngine:
 
     @staticmethod
     def _capture(plan, dev):
-        """One HIP graph of the whole plan (side lanes become parallel branches of the graph)."""
+        """One HIP graph of the whole plan (side lanes become parallel branches of the graph).
+
+        The side lane's stream has normal priority.  With a high-priority side stream (round 2), engines built
+        later in the same process replayed their graph at ~1,750 instead of ~2,930 bursts/s, run after run;
+        at priority 0 six engines in a row all ran at 2,919-2,935.  Per-lane graphs replayed on the plan's
+        own streams were stable as well but ~2.5 % slower (tools/lane_ab.py)."""
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             plan.run(L.stream_ptr(dev))
