@@ -1332,6 +1332,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ws_kernel(ConvK k, int tiles_x
         const int off = (((t.y0 + pp / TW) * k.out_w + t.x0 + pp % TW) * k.r_ld + r_cb + ls * 8) * (int)sizeof(T);
         blds16(buf_rsrc((const T*)k.r + t.r_off, rframe_bytes), off, 0, lres + buf * C::RES_U4 + q * 64);
     };
+    u32x4_t packed[C::GW];
+    // bias + act (+ residual from the LDS + post-act, + gate) of a finished tile into `packed`
     auto epilogue = [&](const Tile& t, int rbuf) {
         u32x4_t gatev[EPI == 5 ? C::GW : 1];
         if constexpr (EPI == 5) {
@@ -1367,11 +1369,16 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ws_kernel(ConvK k, int tiles_x
                     v[2 * e + 1] = H16<T>::hi(gatev[j][e]) > 0.f ? v[2 * e + 1] : 0.f;
                 }
             }
-            u32x4_t o;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) o[e] = H16<T>::pack(v[2 * e], v[2 * e + 1]);
-            if (cout_ok) *(u32x4_t*)((T*)k.y + t.y_off + px_off(j) * k.y_ld + 8 * g) = o;
+            for (int e = 0; e < 4; ++e) packed[j][e] = H16<T>::pack(v[2 * e], v[2 * e + 1]);
         }
+    };
+    // the tile's packed outputs, stored right after the next barrier (issued before it, the stores would
+    // hold up that barrier's vmcnt(0))
+    auto store = [&](const Tile& t) {
+#pragma unroll
+        for (int j = 0; j < C::GW; ++j)
+            if (cout_ok) *(u32x4_t*)((T*)k.y + t.y_off + px_off(j) * k.y_ld + 8 * g) = packed[j];
     };
 
     Tile cur = decode(0), prev = cur;
@@ -1400,8 +1407,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ws_kernel(ConvK k, int tiles_x
 #endif
         __syncthreads();                // this tile's halo landed (vmcnt(0) + barrier); the other buffer is free
         PIPE_STAMP(5 + ti * 5);
-        const bool fin = ti > 0, more = ti + 1 < my_tiles;
-        if (fin) epilogue(prev, (ti - 1) & 1);   // previous tile: accumulators + residual -> outputs
+        const bool more = ti + 1 < my_tiles;
+        if (ti > 0) store(prev);        // previous tile's outputs (computed before the barrier)
         PIPE_STAMP(6 + ti * 5);
         const Tile nxt = more ? decode(ti + 1) : cur;
         const u32x4_t* lb = lds + (ti & 1) * C::STAGE_U4;
@@ -1448,11 +1455,21 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ws_kernel(ConvK k, int tiles_x
             }
         }
         PIPE_STAMP(7 + ti * 5);
+        // this tile's epilogue before the next barrier: the waves that finish their MFMAs first fill the
+        // barrier skew with it.  Its residual landed before this tile's barrier -- except tile 0's, which other
+        // waves DMA'd during its k-steps (one extra barrier); buffer ti & 1 is next written by the DMA of tile
+        // ti + 2's residual, issued after the next barrier
+        if constexpr (RES_BUFS > 0) {
+            if (has_res && ti == 0) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+            }
+        }
+        epilogue(cur, ti & 1);
         prev = cur;
         cur = nxt;
     }
-    __syncthreads();                    // the last tile's residual landed
-    epilogue(prev, (my_tiles - 1) & 1);
+    store(prev);
     PIPE_STAMP(1);
 }
 
