@@ -15,6 +15,7 @@ SHAPES = [  # name, frames, H, W, cin, cout, k
     ('wp.out 128->512', 112, 48, 48, 128, 512, 3),
     ('dec.post 32->32', 8, 384, 384, 32, 32, 3),
     ('dec.pre 64->64', 8, 48, 48, 64, 64, 3),
+    ('dec.init 512->64', 8, 48, 48, 512, 64, 3),
     ('enc.init 4->64', 112, 48, 48, 4, 64, 3),
     ('proj 512->64 1x1', 104, 48, 48, 512, 64, 1),
     ('pwc.dec2.d4 544->32', 104, 16, 16, 544, 32, 3),
