@@ -330,6 +330,113 @@ __global__ __launch_bounds__(256) void conv_splitk_finalize(ConvK k) {
     epilogue_px<T>(k, p, co, a, load_bias4(k, co));
 }
 
+// ------------------------------------------------------------------------------------------------
+// Narrow-output 3x3 conv over a long K, 16-bit, cout <= 4 (PWC-Net's 2-channel flow head, pwcnet.py:156
+// netFlow: K = 9 x 565 at level 2).  The tiled kernel runs it on 32-cout tiles in 32-channel chunks
+// behind two barriers each: 27 us for 0.5 GFLOP.  Block = 4 waves on a 16 x 4-pixel tile (wave w: tile
+// row w, one 16x16x32 MFMA per (tap, 32 channels); A rows >= cout are the packer's zero padding).  K moves
+// in 64-channel chunks: the chunk's (6 x 18)-pixel halo (whole 128-B pixel pieces) and its 4 weight rows
+// go global -> registers -> one of two LDS buffers, two chunks' loads in flight (two register sets)
+// while the current one is multiplied (one chunk in flight: 19.6 us).
+// Measured and not kept: an MFMA wave streaming its K straight from L2 (16 pixels x 64 B per load,
+// 62 us); lanes over the input channels with v_dot2 (26 us); a block per 16-pixel row with K split over
+// its 4 waves, each staging its own chunks (23.6 us; the refiner's 32-channel output conv 12.5 us
+// against 5.3 us tiled, so convs with cin < 256 stay on the tiled kernel).
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void conv3x3_narrow_kernel(ConvK k, int tiles_x, int tiles_y) {
+    constexpr int TW = 16, TH = 4, HX = TW + 2, NQ = HX * (TH + 2);     // 108 halo pixels
+    constexpr int GPC = 8;                                               // 8-channel groups per chunk
+    constexpr int NCO = 4;                                               // weight rows staged
+    constexpr int HALO_ITEMS = NQ * GPC, W_ITEMS = NCO * 9 * GPC, ITEMS = HALO_ITEMS + W_ITEMS;
+    constexpr int PER = (ITEMS + 255) / 256;
+    constexpr int PITCH = GPC + 1;                                       // 16-B slots per halo pixel (+1: banks)
+    constexpr int BUF = NQ * PITCH + W_ITEMS;                            // 16-B slots per buffer
+    __shared__ __attribute__((aligned(16))) u32x4_t lds[2][BUF];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int col = lane & 15, kgl = lane >> 4;
+    int b = blockIdx.x;
+    const int tx = b % tiles_x; b /= tiles_x;
+    const int ty = b % tiles_y;
+    const int f = b / tiles_y;
+    const T* xb = (const T*)k.x + map_frame(k.xm, f) * k.x_is;
+    const int y0 = ty * TH - 1, x0 = tx * TW - 1;
+    const int nchunk = (k.CG + GPC - 1) / GPC;
+
+    // two register sets: chunk c + 1 lands in one while chunk c + 2's loads go out into the other
+    u32x4_t ra[PER], rb[PER];
+    auto load = [&](int c, u32x4_t (&r)[PER]) {
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int it = tid + 256 * i;
+            u32x4_t v = {0u, 0u, 0u, 0u};
+            if (c < nchunk && it < HALO_ITEMS) {
+                const int q = it / GPC, gg = it - q * GPC;
+                const int hy = q / HX, hx = q - hy * HX;
+                const int iy = y0 + hy, ix = x0 + hx, g = c * GPC + gg;
+                if (g < k.CG && (unsigned)iy < (unsigned)k.in_h && (unsigned)ix < (unsigned)k.in_w)
+                    v = *(const u32x4_t*)(xb + ((long long)iy * k.in_w + ix) * k.x_ld + g * 8);
+            } else if (c < nchunk && it < ITEMS) {
+                const int wi = it - HALO_ITEMS;
+                const int co = wi / (9 * GPC), rest = wi - co * (9 * GPC);
+                const int tap = rest / GPC, gg = rest - tap * GPC, g = c * GPC + gg;
+                if (g < k.CG) v = *(const u32x4_t*)((const T*)k.w + (long long)co * k.Kp + (tap * k.CG + g) * 8);
+            }
+            r[i] = v;
+        }
+    };
+    auto put = [&](int buf, const u32x4_t (&r)[PER]) {
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int it = tid + 256 * i;
+            if (it < HALO_ITEMS) {
+                const int q = it / GPC, gg = it - q * GPC;
+                lds[buf][q * PITCH + gg] = r[i];
+            } else if (it < ITEMS) {
+                lds[buf][NQ * PITCH + (it - HALO_ITEMS)] = r[i];
+            }
+        }
+    };
+    f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+    auto compute = [&](int c) {
+        const u32x4_t* L = lds[c & 1];
+        const int gcount = min(GPC, k.CG - c * GPC);                     // 8, or 4 in a 32-channel tail chunk
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+            const int ky = tap / 3, kx = tap % 3;
+            const int q = (wave + ky) * HX + col + kx;
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                if (s * 4 >= gcount) break;
+                Frag<T> A, B;
+                B.v = __builtin_bit_cast(bf16x8_t, L[q * PITCH + s * 4 + kgl]);
+                if (col < NCO) A.v = __builtin_bit_cast(bf16x8_t, L[NQ * PITCH + (col * 9 + tap) * GPC + s * 4 + kgl]);
+                else A.zero();
+                acc = mma(A, B, acc);
+            }
+        }
+    };
+    // step c: chunk c + 1 is in flight in `nxt`, `fre` is free; chunk c + 2 goes out into `fre`, chunk c
+    // is multiplied from LDS, then chunk c + 1 is written to the other buffer
+    auto step = [&](int c, u32x4_t (&nxt)[PER], u32x4_t (&fre)[PER]) {
+        load(c + 2, fre);
+        compute(c);
+        if (c + 1 < nchunk) put((c + 1) & 1, nxt);
+        __syncthreads();
+    };
+    load(0, rb);
+    load(1, ra);
+    put(0, rb);
+    __syncthreads();
+    for (int c = 0; c < nchunk; c += 2) {
+        step(c, ra, rb);
+        if (c + 1 < nchunk) step(c + 1, rb, ra);
+    }
+    const int oy = ty * TH + wave, ox = tx * TW + col;
+    if (kgl != 0 || oy >= k.out_h || ox >= k.out_w) return;
+    epilogue_px<T>(k, (f * k.out_h + oy) * k.out_w + ox, 0, acc, load_bias4(k, 0));
+}
+
 // row layout [cout_pad][Kp] -> chunk-major pieces [cout_pad/16][chunk][tap][g][16 co][8] (3x3, cin > 16);
 // within each tile of P = (cout <= 32 ? 32 : 64) couts, row col of 16-cout block blk holds physical cout
 // pipe_cout_perm(blk, col) (the pipelined kernel's 8-consecutive-couts-per-lane epilogue order)
@@ -1596,6 +1703,24 @@ void pick_generic_tile(const ConvK& k, int& best_m, int& best_n) {
     }
 }
 
+// narrow-output 3x3 convs over a long K (conv3x3_narrow_kernel): 16-bit 3x3/s1/p1/d1, cout <= 4, cin >= 256,
+// NHWC output without gate
+int g_narrow_enabled = 1;
+bool use_narrow(const dbsr_conv_desc* d) {
+    return g_narrow_enabled && is16(d->x.dtype) && !d->precise && d->kh == 3 && d->kw == 3 && d->stride == 1 &&
+           d->pad == 1 && d->dil == 1 && d->cout <= 4 && d->cin >= 256 && d->out_mode == DBSR_OUT_NHWC &&
+           !d->gate.ptr;
+}
+template <typename T>
+int launch_narrow(const ConvK& k, const dbsr_conv_desc* d, hipStream_t s) {
+    const int tiles_x = (d->out_w + 15) / 16, tiles_y = (d->out_h + 3) / 4;
+    const long long blocks = (long long)d->n_frames * tiles_x * tiles_y;
+    DBSR_CHECK_ARG(blocks < (1LL << 31), "conv2d: too many narrow tiles");
+    hipLaunchKernelGGL((conv3x3_narrow_kernel<T>), dim3((unsigned)blocks), dim3(256), 0, s, k, tiles_x, tiles_y);
+    DBSR_LAUNCH_CHECK();
+    return 0;
+}
+
 // 3x3 'same' convolutions (pad == dilation) with dilation 1/2/4/8 (the PWC refiner's context
 // network, pwcnet.py:227-241, has 2/4/8; fp32 tiles with dilation 8 exceed the LDS)
 bool use_tiled(const dbsr_conv_desc* d) {
@@ -1647,6 +1772,7 @@ int dispatch_conv(const ConvK& k, const dbsr_conv_desc* d, hipStream_t s) {
         if (px) return dispatch_ws<T>(px, k, d, s);
         const int cfg = pick_pipe(d);
         if (cfg) return dispatch_pipe<T>(cfg, k, d, s);
+        if (use_narrow(d)) return launch_narrow<T>(k, d, s);
     }
     if (use_tiled(d)) {
         switch (d->dil) {
@@ -1984,6 +2110,7 @@ extern "C" int dbsr_conv_kernel_for(const dbsr_conv_desc* d) {
     if (pick_pipe(d)) return 2;
     if (use_upsample(d, make_convk(d))) return 3;
     if (use_pointwise(d)) return 5;
+    if (use_narrow(d)) return 6;
     return use_tiled(d) ? 1 : 0;
 }
 
@@ -1994,7 +2121,7 @@ extern "C" int dbsr_conv_head_ok(const dbsr_conv_desc* d) {
 
 extern "C" size_t dbsr_conv_workspace_bytes(const dbsr_conv_desc* d) {
     if (!d || pick_ws(d) || pick_pipe(d) || use_tiled(d) || d->precise || use_upsample(d, make_convk(d)) ||
-        use_pointwise(d))
+        use_pointwise(d) || use_narrow(d))
         return 0;
     const ConvK k = make_convk(d);
     int m, n;
@@ -2008,6 +2135,7 @@ extern "C" int dbsr_set_conv_algo(int algo) {
     g_tiled_enabled = algo >= 1;
     g_pipe_enabled = algo == 3 ? 2 : algo >= 2 ? 1 : 0;
     g_ws_enabled = algo == 2;
+    g_narrow_enabled = algo >= 2;
     return 0;
 }
 

@@ -113,7 +113,7 @@ int dbsr_set_conv_algo(int algo);
 /* Which kernel dbsr_conv2d would launch for `d` under the current selection: 5 pointwise projection
  * (16-bit 1x1, cin 32..512 a power of two, cout 32 | 64, no residual: merging.py:34), 4 weight-stationary,
  * 3 PixelShuffle upsampler (bf16 1x1 with DBSR_OUT_SHUFFLE, 32 channels per sub-pixel), 2 pipelined,
- * 1 LDS-tiled, 0 generic. */
+ * 6 narrow-output 3x3 (16-bit, cout <= 4, cin >= 256, pad 1: the PWC level-2 flow head), 1 LDS-tiled, 0 generic. */
 int dbsr_conv_kernel_for(const dbsr_conv_desc* d);
 /* A 32-channel ResBlock conv2 fused with a 1x1 head (the decoder's last post-ResBlock + RGB predictor,
  * decoders.py:59-61 / blocks.py:94-96): t = ReLU(conv(x) + bias + residual) stays in registers (d->y is

@@ -291,6 +291,38 @@ def test_conv1x1_pointwise(ops, case):
     np.testing.assert_allclose(outs[2].numpy(), outs[0].numpy(), atol=1e-2, rtol=8e-3)
 
 
+@pytest.mark.parametrize('dt', [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize('case', [(3, 565, 16, 16, 2, 1, False),    # PWC level-2 flow head (pwcnet.py:156)
+                                  (2, 256, 16, 16, 2, 1, True),     # the smallest K served (4 chunks), residual
+                                  (2, 400, 13, 11, 3, 1, True),     # ragged tiles, residual, 32-channel tail chunk
+                                  (1, 272, 9, 20, 4, 1, False),     # two 16-pixel tiles across, the last partial
+                                  (2, 1000, 5, 7, 1, 1, False)])    # 16 chunks, one output channel
+def test_conv3x3_narrow(ops, dt, case):
+    """Narrow-output 3x3 kernel (dbsr_conv_kernel_for == 6, cout <= 4, cin >= 256) against torch fp32 on the same
+    16-bit operands (fp32 output, as the flow heads write it) and against the generic kernel (algo 0)."""
+    from dbsr_amd import _lib
+    N, Cin, H, W, Cout, d, with_res = case
+    gen = torch.Generator().manual_seed(Cin * 10 + Cout + H)
+    x = torch.randn(N, Cin, H, W, generator=gen)
+    w = torch.randn(Cout, Cin, 3, 3, generator=gen) / (Cin * 9) ** 0.5
+    b = torch.randn(Cout, generator=gen) * 0.1
+    res = torch.randn(N, Cout, H, W, generator=gen) if with_res else None
+    ref = F.conv2d(x.to(dt).float(), w.to(dt).float(), b, padding=d, dilation=d)
+    if with_res:
+        ref = ref + res
+    outs = {}
+    try:
+        for algo in (2, 0):
+            _lib.lib().dbsr_set_conv_algo(algo)
+            outs[algo] = ops.conv2d(x.to(DEV), w.to(DEV), b.to(DEV), padding=d, dilation=d, compute_dtype=dt,
+                                    out_f32=True, residual=res.to(DEV) if with_res else None).cpu()
+            assert ops.conv2d.last_kernel == (6 if algo == 2 else 0)
+    finally:
+        _lib.lib().dbsr_set_conv_algo(2)
+    np.testing.assert_allclose(outs[2].numpy(), ref.numpy(), atol=1e-4, rtol=1e-4)
+    np.testing.assert_allclose(outs[2].numpy(), outs[0].numpy(), atol=1e-4, rtol=1e-4)
+
+
 @pytest.mark.parametrize('dt', [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize('shape', [(2, 32, 384, 384), (1, 16, 13, 21), (3, 8, 9, 4)])
 def test_gauss_blur3(shape, dt):

@@ -24,7 +24,8 @@ KERNELS = {   # label -> (name predicate, algorithmic bytes per launch at the de
 
 # kernel name -> bench.py family (bench.py CONV_FAMILIES / roofline_hbm keys)
 FAMILY = [('conv3x3_ws_kernel', 'conv3x3_ws'), ('conv3x3_pipe_kernel', 'conv3x3_pipe'),
-          ('conv3x3_tiled_kernel', 'conv3x3_tiled'), ('conv1x1_kernel', 'conv1x1'),
+          ('conv3x3_tiled_kernel', 'conv3x3_tiled'), ('conv3x3_narrow_kernel', 'conv3x3_narrow'),
+          ('conv1x1_kernel', 'conv1x1'),
           ('upsample_shuffle_kernel', 'conv1x1_shuffle'), ('pwc_dense', 'pwc_dense'),
           ('pwc_extract_kernel', 'pwc_extract'), ('warp512_bf16_kernel', 'warp'), ('fuse512_bf16_kernel', 'fuse')]
 
