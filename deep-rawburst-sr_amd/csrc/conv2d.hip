@@ -336,12 +336,13 @@ __global__ __launch_bounds__(256) void conv_splitk_finalize(ConvK k) {
 // behind two barriers each: 27 us for 0.5 GFLOP.  Block = 4 waves on a 16 x 4-pixel tile (wave w: tile
 // row w, one 16x16x32 MFMA per (tap, 32 channels); A rows >= cout are the packer's zero padding).  K moves
 // in 64-channel chunks: the chunk's (6 x 18)-pixel halo (whole 128-B pixel pieces) and its 4 weight rows
-// go global -> registers -> one of two LDS buffers, two chunks' loads in flight (two register sets)
-// while the current one is multiplied (one chunk in flight: 19.6 us).
+// go global -> registers -> one of two LDS buffers, the next chunk's loads in flight while the current
+// one is multiplied: 19.6 us.
 // Measured and not kept: an MFMA wave streaming its K straight from L2 (16 pixels x 64 B per load,
 // 62 us); lanes over the input channels with v_dot2 (26 us); a block per 16-pixel row with K split over
 // its 4 waves, each staging its own chunks (23.6 us; the refiner's 32-channel output conv 12.5 us
-// against 5.3 us tiled, so convs with cin < 256 stay on the tiled kernel).
+// against 5.3 us tiled, so convs with cin < 256 stay on the tiled kernel); two chunks in flight here
+// (two register sets) 21.2 us.
 // ------------------------------------------------------------------------------------------------
 template <typename T>
 __global__ __launch_bounds__(256) void conv3x3_narrow_kernel(ConvK k, int tiles_x, int tiles_y) {
@@ -363,20 +364,19 @@ __global__ __launch_bounds__(256) void conv3x3_narrow_kernel(ConvK k, int tiles_
     const int y0 = ty * TH - 1, x0 = tx * TW - 1;
     const int nchunk = (k.CG + GPC - 1) / GPC;
 
-    // two register sets: chunk c + 1 lands in one while chunk c + 2's loads go out into the other
-    u32x4_t ra[PER], rb[PER];
-    auto load = [&](int c, u32x4_t (&r)[PER]) {
+    u32x4_t r[PER];
+    auto load = [&](int c) {
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
             const int it = tid + 256 * i;
             u32x4_t v = {0u, 0u, 0u, 0u};
-            if (c < nchunk && it < HALO_ITEMS) {
+            if (it < HALO_ITEMS) {
                 const int q = it / GPC, gg = it - q * GPC;
                 const int hy = q / HX, hx = q - hy * HX;
                 const int iy = y0 + hy, ix = x0 + hx, g = c * GPC + gg;
                 if (g < k.CG && (unsigned)iy < (unsigned)k.in_h && (unsigned)ix < (unsigned)k.in_w)
                     v = *(const u32x4_t*)(xb + ((long long)iy * k.in_w + ix) * k.x_ld + g * 8);
-            } else if (c < nchunk && it < ITEMS) {
+            } else if (it < ITEMS) {
                 const int wi = it - HALO_ITEMS;
                 const int co = wi / (9 * GPC), rest = wi - co * (9 * GPC);
                 const int tap = rest / GPC, gg = rest - tap * GPC, g = c * GPC + gg;
@@ -385,7 +385,7 @@ __global__ __launch_bounds__(256) void conv3x3_narrow_kernel(ConvK k, int tiles_
             r[i] = v;
         }
     };
-    auto put = [&](int buf, const u32x4_t (&r)[PER]) {
+    auto put = [&](int buf) {
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
             const int it = tid + 256 * i;
@@ -398,7 +398,11 @@ __global__ __launch_bounds__(256) void conv3x3_narrow_kernel(ConvK k, int tiles_
         }
     };
     f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
-    auto compute = [&](int c) {
+    load(0);
+    put(0);
+    __syncthreads();
+    for (int c = 0; c < nchunk; ++c) {
+        if (c + 1 < nchunk) load(c + 1);
         const u32x4_t* L = lds[c & 1];
         const int gcount = min(GPC, k.CG - c * GPC);                     // 8, or 4 in a 32-channel tail chunk
 #pragma unroll
@@ -415,22 +419,8 @@ __global__ __launch_bounds__(256) void conv3x3_narrow_kernel(ConvK k, int tiles_
                 acc = mma(A, B, acc);
             }
         }
-    };
-    // step c: chunk c + 1 is in flight in `nxt`, `fre` is free; chunk c + 2 goes out into `fre`, chunk c
-    // is multiplied from LDS, then chunk c + 1 is written to the other buffer
-    auto step = [&](int c, u32x4_t (&nxt)[PER], u32x4_t (&fre)[PER]) {
-        load(c + 2, fre);
-        compute(c);
-        if (c + 1 < nchunk) put((c + 1) & 1, nxt);
+        if (c + 1 < nchunk) put((c + 1) & 1);
         __syncthreads();
-    };
-    load(0, rb);
-    load(1, ra);
-    put(0, rb);
-    __syncthreads();
-    for (int c = 0; c < nchunk; c += 2) {
-        step(c, ra, rb);
-        if (c + 1 < nchunk) step(c + 1, rb, ra);
     }
     const int oy = ty * TH + wave, ox = tx * TW + col;
     if (kgl != 0 || oy >= k.out_h || ox >= k.out_w) return;
