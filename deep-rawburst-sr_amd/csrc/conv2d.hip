@@ -1575,6 +1575,12 @@ int g_ws_enabled = 1;
 // either 16 < cin <= 64, 32 < cout <= 512 on 16x16 tiles (WM 64) or 16 < cin <= 32, 16 <= cout <= 32 on 64x8
 // tiles (WM 32: the decoder's 384x384 post-ResBlocks), aligned NHWC output / residual
 inline bool ws_narrow(const dbsr_conv_desc* d) { return d->cout <= 32; }
+// 16x8 instead of 16x16 tiles (WM 64, 32 < cin <= 64) when the 16x16 grid would cover under half the chip:
+// the decoder's pre-ResBlocks (8 frames of 48x48: 72 tiles) are a block's weight staging plus one tile
+inline bool ws_short(const dbsr_conv_desc* d) {
+    return !ws_narrow(d) && d->cin > 32 && d->out_w % 16 == 0 && d->out_h % 16 == 0 &&
+           (long long)d->n_frames * (d->out_w / 16) * (d->out_h / 16) * ((d->cout + 63) / 64) < 128;
+}
 int pick_ws(const dbsr_conv_desc* d) {
     if (!g_ws_enabled || !is16(d->x.dtype) || d->precise || d->kh != 3 || d->kw != 3 || d->stride != 1 ||
         d->pad != 1 || d->dil != 1 || d->cin <= 16 || d->cin > 64 || d->out_mode != DBSR_OUT_NHWC ||
@@ -1585,7 +1591,7 @@ int pick_ws(const dbsr_conv_desc* d) {
         (d->res.ptr && (d->res.ld % 8 || d->res.c0 % 8)))
         return 0;
     const bool narrow = ws_narrow(d);
-    const int tw = narrow ? 64 : 16, th = narrow ? 8 : 16, wm = narrow ? 32 : 64;
+    const int tw = narrow ? 64 : 16, th = (narrow || ws_short(d)) ? 8 : 16, wm = narrow ? 32 : 64;
     if (narrow && (d->cout < 16 || d->cin > 32)) return 0;      // WM 32: one 32-channel chunk (LDS budget)
     if (d->out_w % tw || d->out_h % th) return 0;
     if ((long long)d->in_h * d->in_w * d->x.ld * 2 >= (1LL << 31)) return 0;   // 32-bit buffer offsets per frame
@@ -1627,6 +1633,7 @@ int launch_ws(const ConvK& k, const dbsr_conv_desc* d, int px, hipStream_t s) {
 template <typename T>
 int dispatch_ws(int px, const ConvK& k, const dbsr_conv_desc* d, hipStream_t s) {
     if (ws_narrow(d)) return launch_ws<T, 32, 64, 8, 1>(k, d, px, s);
+    if (ws_short(d)) return launch_ws<T, 64, 16, 8, 2>(k, d, px, s);
     if (k.CG / 4 == 1) return launch_ws<T, 64, 16, 16, 1>(k, d, px, s);
     return launch_ws<T, 64, 16, 16, 2>(k, d, px, s);
 }

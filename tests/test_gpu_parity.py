@@ -231,11 +231,12 @@ WS32_EPI = [
 @pytest.mark.parametrize('case', WS_EPI + WS32_EPI)
 def test_ws_conv_variants(ops_mod, case):
     """Weight-stationary 3x3 conv against torch on the same 16-bit-rounded operands, and against the
-    generic kernel; WM 64: frames 48x48 (the encoder's) and 32x16 (non-square, edge tiles on both axes);
+    generic kernel; WM 64: frames 48x48 (the encoder's) and 32x16 (non-square, edge tiles on both axes),
+    on 16x8 tiles where the 16x16 grid is under 128 tiles (12 and 40 frames at cin > 32) and on 16x16 tiles;
     WM 32 (cout <= 32, 64x8 tiles): 64x64 and 48x192 frames."""
     from dbsr_amd import _lib
     act, use_res, post, cin, cout, dt = case
-    shapes = ((12, 48, 48), (40, 32, 16)) if cout > 32 else ((8, 64, 64), (4, 48, 192))
+    shapes = ((12, 48, 48), (40, 32, 16), (26, 48, 48)) if cout > 32 else ((8, 64, 64), (4, 48, 192))
     for (N, H, W) in shapes:
         gen = torch.Generator().manual_seed(cin * 13 + cout + act * 7 + post + H)
         x = torch.randn(N, cin, H, W, generator=gen)
