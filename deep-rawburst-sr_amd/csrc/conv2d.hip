@@ -55,6 +55,17 @@ struct ConvK {
     int stage_epi;       // generic kernel, MT == 4: LDS-staged 16-B-row epilogue (set by launch_conv)
 };
 
+// The geometry every dispatch decision is taken on: `d` itself, or (d->plan_h > 0) `d` as if its image were
+// plan_h output rows tall -- a frame-sharded rank's decoder slab then takes the whole image's kernels, tiles
+// and K split, so each of its output pixels is summed in the whole image's order (dbsr_hip.h: plan_h)
+const dbsr_conv_desc* sel_view(const dbsr_conv_desc* d, dbsr_conv_desc& v) {
+    if (d->plan_h <= 0 || d->plan_h == d->out_h) return d;
+    v = *d;
+    v.in_h = d->in_h + (d->plan_h - d->out_h) * d->stride;
+    v.out_h = d->plan_h;
+    return &v;
+}
+
 template <typename T> struct Frag;
 template <> struct Frag<bf16_t> {
     bf16x8_t v;
@@ -1251,6 +1262,11 @@ int pick_pipe(const dbsr_conv_desc* d) {
     const long long nt = (long long)d->n_frames * (d->out_w / tw) * (d->out_h / th) * ((d->cout + wm - 1) / wm);
     return (nt >= (cfg == 3 ? 64 : 256) || g_pipe_enabled == 2) ? cfg : 0;
 }
+// a plan_h slab `g` can run pipelined tile `cfg` (chosen for the whole image)
+bool pipe_fits(int cfg, const dbsr_conv_desc* g) {
+    if (cfg == 3) return g->out_h == 16;
+    return g->out_h % (cfg == 4 ? 16 : 8) == 0;
+}
 
 // ------------------------------------------------------------------------------------------------
 // Weight-stationary 3x3 conv for Cin <= 64 (the encoder and offset-feature ResNets and enc.out at
@@ -1581,7 +1597,9 @@ inline bool ws_short(const dbsr_conv_desc* d) {
     return !ws_narrow(d) && d->cin > 32 && d->out_w % 16 == 0 && d->out_h % 16 == 0 &&
            (long long)d->n_frames * (d->out_w / 16) * (d->out_h / 16) * ((d->cout + 63) / 64) < 128;
 }
-int pick_ws(const dbsr_conv_desc* d) {
+// (d: the selection view; g: the launch geometry when it differs -- a plan_h slab -- which must suit the tile
+// chosen for d; the block count then follows g's own tile count)
+int pick_ws(const dbsr_conv_desc* d, const dbsr_conv_desc* g = nullptr) {
     if (!g_ws_enabled || !is16(d->x.dtype) || d->precise || d->kh != 3 || d->kw != 3 || d->stride != 1 ||
         d->pad != 1 || d->dil != 1 || d->cin <= 16 || d->cin > 64 || d->out_mode != DBSR_OUT_NHWC ||
         d->y.dtype != d->x.dtype)
@@ -1599,9 +1617,12 @@ int pick_ws(const dbsr_conv_desc* d) {
     const int nct = (d->cout + wm - 1) / wm;
     const long long nsp = (long long)d->n_frames * (d->out_w / tw) * (d->out_h / th);
     const int cus = d->max_blocks > 0 ? std::min(d->max_blocks, num_cus()) : num_cus();
-    const long long want = (nsp + 7) / 8;                                      // spatial streams per XCD
-    const long long spx = std::min<long long>(cus / 8 / nct, want);
-    if (spx < 1 || nsp * nct < 64) return 0;
+    if (cus / 8 / nct < 1 || nsp * nct < 64) return 0;
+    if (!g) g = d;
+    if (g->out_h % th) return -1;                                             // slab rows do not tile
+    const long long nsp_g = (long long)g->n_frames * (g->out_w / tw) * (g->out_h / th);
+    const long long want = (nsp_g + 7) / 8;                                   // spatial streams per XCD
+    const long long spx = std::max<long long>(1, std::min<long long>(cus / 8 / nct, want));
     return (int)(spx * nct);
 }
 
@@ -1631,9 +1652,9 @@ int launch_ws(const ConvK& k, const dbsr_conv_desc* d, int px, hipStream_t s) {
 }
 
 template <typename T>
-int dispatch_ws(int px, const ConvK& k, const dbsr_conv_desc* d, hipStream_t s) {
-    if (ws_narrow(d)) return launch_ws<T, 32, 64, 8, 1>(k, d, px, s);
-    if (ws_short(d)) return launch_ws<T, 64, 16, 8, 2>(k, d, px, s);
+int dispatch_ws(int px, const ConvK& k, const dbsr_conv_desc* d, const dbsr_conv_desc* sel, hipStream_t s) {
+    if (ws_narrow(sel)) return launch_ws<T, 32, 64, 8, 1>(k, d, px, s);
+    if (ws_short(sel)) return launch_ws<T, 64, 16, 8, 2>(k, d, px, s);
     if (k.CG / 4 == 1) return launch_ws<T, 64, 16, 16, 1>(k, d, px, s);
     return launch_ws<T, 64, 16, 16, 2>(k, d, px, s);
 }
@@ -1738,7 +1759,7 @@ int tiled_blocks(const dbsr_conv_desc* d, int wm, int wn) {
 #ifndef DBSR_TILE_WM32_MAX_COUT
 #define DBSR_TILE_WM32_MAX_COUT 64      // wider convs keep 64-cout tiles (halving re-reads the halo twice)
 #endif
-void pick_tiled_tile(const dbsr_conv_desc* d, int& wm, int& wn) {
+void pick_tiled_tile(const dbsr_conv_desc* d, int& wm, int& wn) {     // (d: the selection view)
     wm = d->cout <= 32 ? 32 : 64;
     wn = (wm == 32 && d->out_h >= 32) ? 128 : 64;
     if (tiled_blocks(d, wm, wn) >= 512) return;
@@ -1753,39 +1774,51 @@ void pick_tiled_tile(const dbsr_conv_desc* d, int& wm, int& wn) {
 }
 
 template <typename T, int D>
-int dispatch_tiled_d(const ConvK& k, const dbsr_conv_desc* d, hipStream_t s) {
+int dispatch_tiled_d(const ConvK& k, const dbsr_conv_desc* d, const dbsr_conv_desc* sel, hipStream_t s) {
     int wm, wn;
-    pick_tiled_tile(d, wm, wn);
+    pick_tiled_tile(sel, wm, wn);
     if (wm == 64) return launch_tiled<T, 64, 64, D>(k, d->n_frames, s);
     if (wn == 128) return launch_tiled<T, 32, 128, D>(k, d->n_frames, s);
     if (wn == 64) return launch_tiled<T, 32, 64, D>(k, d->n_frames, s);
     return launch_tiled<T, 32, 16, D>(k, d->n_frames, s);
 }
 
+ConvK make_convk(const dbsr_conv_desc* d);
+
+int slab_misfit(const dbsr_conv_desc* d, const dbsr_conv_desc* sel) {
+    dbsr_set_error("conv2d: a %d-row slab cannot take the tile chosen for plan_h = %d rows (use a multiple of 16)",
+                   d->out_h, sel->out_h);
+    return DBSR_E_ARG;
+}
+
+// d: the launch geometry; sel: the selection view (sel_view)
 template <typename T>
-int dispatch_conv(const ConvK& k, const dbsr_conv_desc* d, hipStream_t s) {
+int dispatch_conv(const ConvK& k, const dbsr_conv_desc* d, const dbsr_conv_desc* sel, hipStream_t s) {
     if constexpr (sizeof(T) == 2) {
-        const int px = pick_ws(d);
-        if (px) return dispatch_ws<T>(px, k, d, s);
-        const int cfg = pick_pipe(d);
+        const int px = pick_ws(sel, d);
+        if (px < 0) return slab_misfit(d, sel);
+        if (px) return dispatch_ws<T>(px, k, d, sel, s);
+        const int cfg = pick_pipe(sel);
+        if (cfg && !pipe_fits(cfg, d)) return slab_misfit(d, sel);
         if (cfg) return dispatch_pipe<T>(cfg, k, d, s);
-        if (use_narrow(d)) return launch_narrow<T>(k, d, s);
+        if (use_narrow(sel)) return launch_narrow<T>(k, d, s);
     }
-    if (use_tiled(d)) {
+    if (use_tiled(sel)) {
         switch (d->dil) {
-            case 1: return dispatch_tiled_d<T, 1>(k, d, s);
-            case 2: return dispatch_tiled_d<T, 2>(k, d, s);
-            case 4: return dispatch_tiled_d<T, 4>(k, d, s);
+            case 1: return dispatch_tiled_d<T, 1>(k, d, sel, s);
+            case 2: return dispatch_tiled_d<T, 2>(k, d, sel, s);
+            case 4: return dispatch_tiled_d<T, 4>(k, d, sel, s);
             default:
-                if constexpr (sizeof(T) == 2) return dispatch_tiled_d<T, 8>(k, d, s);
+                if constexpr (sizeof(T) == 2) return dispatch_tiled_d<T, 8>(k, d, sel, s);
                 dbsr_set_error("conv2d: no fp32 tile for dilation %d", d->dil);
                 return DBSR_E_ARG;
         }
     }
     int best_m, best_n;
-    pick_generic_tile(k, best_m, best_n);
+    const ConvK ksel = sel == d ? k : make_convk(sel);
+    pick_generic_tile(ksel, best_m, best_n);
     ConvK kk = k;
-    kk.ksplit = choose_ksplit(k, best_m, best_n);
+    kk.ksplit = choose_ksplit(ksel, best_m, best_n);
     if (kk.ksplit > 1 && splitk_bytes(k, kk.ksplit) > d->workspace_bytes) kk.ksplit = 1;
 #define DBSR_CONV_CASE(M, N) if (best_m == M && best_n == N) return launch_conv<T, M, N>(kk, s);
     DBSR_CONV_CASE(4, 4) DBSR_CONV_CASE(4, 2) DBSR_CONV_CASE(4, 1)
@@ -2101,29 +2134,67 @@ extern "C" int dbsr_diag_pipe_stamps(unsigned long long* host, long long n) {
 }
 #endif
 
+// the order dbsr_conv2d tries the kernels in, on the selection view (16-bit kernels first)
+int kernel_for(const dbsr_conv_desc* d) {
+    dbsr_conv_desc v;
+    const dbsr_conv_desc* sel = sel_view(d, v);
+    if (d->precise) return 0;
+    if (use_upsample(sel, make_convk(sel))) return 3;
+    if (use_pointwise(sel)) return 5;
+    if (is16(d->x.dtype)) {
+        if (pick_ws(sel)) return 4;
+        if (pick_pipe(sel)) return 2;
+        if (use_narrow(sel)) return 6;
+    }
+    return use_tiled(sel) ? 1 : 0;
+}
+
 extern "C" int dbsr_conv_kernel_for(const dbsr_conv_desc* d) {
+    return d ? kernel_for(d) : -1;
+}
+
+extern "C" int dbsr_conv_dispatch_variant(const dbsr_conv_desc* d) {
     if (!d) return -1;
-    if (pick_ws(d)) return 4;
-    if (pick_pipe(d)) return 2;
-    if (use_upsample(d, make_convk(d))) return 3;
-    if (use_pointwise(d)) return 5;
-    if (use_narrow(d)) return 6;
-    return use_tiled(d) ? 1 : 0;
+    dbsr_conv_desc v;
+    const dbsr_conv_desc* sel = sel_view(d, v);
+    const int kf = kernel_for(d);
+    int var = 0;
+    if (d->precise) {
+        const long long np = (long long)sel->n_frames * sel->out_h * sel->out_w;
+        var = np >= 512 * 256 ? 4 : np >= 512 * 128 ? 2 : 1;
+    } else if (kf == 4) {
+        var = ws_narrow(sel) ? 6408 : ws_short(sel) ? 1608 : 1616;
+    } else if (kf == 2) {
+        var = pick_pipe(sel);
+    } else if (kf == 1) {
+        int wm, wn;
+        pick_tiled_tile(sel, wm, wn);
+        var = wm * 1000 + wn;
+    } else if (kf == 0) {
+        const ConvK k = make_convk(sel);
+        int m, n;
+        pick_generic_tile(k, m, n);
+        var = m * 10000 + n * 1000 + choose_ksplit(k, m, n);
+    }
+    return kf * 1000000 + var;
 }
 
 extern "C" int dbsr_conv_head_ok(const dbsr_conv_desc* d) {
-    return d && pick_pipe(d) == 2 && d->cout == 32 && d->res.ptr && d->act == DBSR_ACT_NONE &&
-           d->post_act == DBSR_ACT_RELU;
+    if (!d) return 0;
+    dbsr_conv_desc v;
+    const dbsr_conv_desc* sel = sel_view(d, v);
+    return pick_pipe(sel) == 2 && pipe_fits(2, d) && d->cout == 32 && d->res.ptr &&
+           d->act == DBSR_ACT_NONE && d->post_act == DBSR_ACT_RELU;
 }
 
 extern "C" size_t dbsr_conv_workspace_bytes(const dbsr_conv_desc* d) {
-    if (!d || pick_ws(d) || pick_pipe(d) || use_tiled(d) || d->precise || use_upsample(d, make_convk(d)) ||
-        use_pointwise(d) || use_narrow(d))
-        return 0;
-    const ConvK k = make_convk(d);
+    if (!d || kernel_for(d) != 0 || d->precise) return 0;
+    dbsr_conv_desc v;
+    const dbsr_conv_desc* sel = sel_view(d, v);
+    const ConvK ksel = make_convk(sel);
     int m, n;
-    pick_generic_tile(k, m, n);
-    return splitk_bytes(k, choose_ksplit(k, m, n));
+    pick_generic_tile(ksel, m, n);
+    return splitk_bytes(make_convk(d), choose_ksplit(ksel, m, n));
 }
 
 extern "C" int dbsr_set_conv_algo(int algo) {
@@ -2198,27 +2269,31 @@ extern "C" int dbsr_conv2d(const dbsr_conv_desc* d, void* stream) {
     const long long npix = (long long)d->n_frames * d->out_h * d->out_w;
     DBSR_CHECK_ARG(npix < (1LL << 31), "conv2d: too many pixels");
 
+    DBSR_CHECK_ARG(d->plan_h >= 0, "conv2d: plan_h must be >= 0");
     ConvK k = make_convk(d);
     hipStream_t s = (hipStream_t)stream;
+    dbsr_conv_desc v;
+    const dbsr_conv_desc* sel = sel_view(d, v);
+    const long long npix_sel = (long long)sel->n_frames * sel->out_h * sel->out_w;
     if (d->precise && d->x.dtype == DBSR_F16) {
         DBSR_CHECK_ARG(d->y.dtype == DBSR_F32 && d->cout <= 16, "conv2d: precise mode needs fp32 output, cout <= 16");
         k.ksplit = 1;
-        if (k.npix >= 512 * 256) return launch_conv<float, 1, 4, f16_t>(k, s);
-        if (k.npix >= 512 * 128) return launch_conv<float, 1, 2, f16_t>(k, s);
+        if (npix_sel >= 512 * 256) return launch_conv<float, 1, 4, f16_t>(k, s);
+        if (npix_sel >= 512 * 128) return launch_conv<float, 1, 2, f16_t>(k, s);
         return launch_conv<float, 1, 1, f16_t>(k, s);
     }
     if (d->precise && d->x.dtype == DBSR_BF16) {
         // bf16 activations, fp32-packed weights, fp32 MFMA: small fp32-output heads (the RGB predictor)
         DBSR_CHECK_ARG(d->y.dtype == DBSR_F32 && d->cout <= 16, "conv2d: precise mode needs fp32 output, cout <= 16");
         k.ksplit = 1;
-        if (k.npix >= 512 * 256) return launch_conv<float, 1, 4, bf16_t>(k, s);
-        if (k.npix >= 512 * 128) return launch_conv<float, 1, 2, bf16_t>(k, s);
+        if (npix_sel >= 512 * 256) return launch_conv<float, 1, 4, bf16_t>(k, s);
+        if (npix_sel >= 512 * 128) return launch_conv<float, 1, 2, bf16_t>(k, s);
         return launch_conv<float, 1, 1, bf16_t>(k, s);
     }
-    if (use_upsample(d, k)) return d->x.dtype == DBSR_F16 ? launch_upsample<f16_t>(k, s) : launch_upsample<bf16_t>(k, s);
-    if (use_pointwise(d)) return d->x.dtype == DBSR_F16 ? launch_pointwise<f16_t>(k, s) : launch_pointwise<bf16_t>(k, s);
-    if (d->x.dtype == DBSR_F16) return dispatch_conv<f16_t>(k, d, s);
-    return d->x.dtype == DBSR_BF16 ? dispatch_conv<bf16_t>(k, d, s) : dispatch_conv<float>(k, d, s);
+    if (use_upsample(sel, k)) return d->x.dtype == DBSR_F16 ? launch_upsample<f16_t>(k, s) : launch_upsample<bf16_t>(k, s);
+    if (use_pointwise(sel)) return d->x.dtype == DBSR_F16 ? launch_pointwise<f16_t>(k, s) : launch_pointwise<bf16_t>(k, s);
+    if (d->x.dtype == DBSR_F16) return dispatch_conv<f16_t>(k, d, sel, s);
+    return d->x.dtype == DBSR_BF16 ? dispatch_conv<bf16_t>(k, d, sel, s) : dispatch_conv<float>(k, d, sel, s);
 }
 
 extern "C" int dbsr_conv2d_head(const dbsr_conv_desc* d, const float* head_w, const float* head_b, int head_cout,

@@ -625,7 +625,9 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(int n, int h, int w, int 
 // (16-B loads of dout[p]), the pixel's few contributions (4 on average) are summed in registers in record
 // order and the result is written once, gated by the encoder output's ReLU (encoders.py:66-72):
 // dfeat[q] = [gate[q] > 0] * sum_p w(p, q) dout[p].  Any flow field costs the same per contribution.  The
-// record order within a pixel follows the scatter's atomics, so fp32 sums are not bitwise reproducible.
+// scatter's atomics place a pixel's records in arbitrary order, so the gather sums them sorted by source pixel
+// (unique within a destination: a source's four taps hit four different pixels): the gradients are bitwise
+// reproducible run to run.
 // ------------------------------------------------------------------------------------------------
 struct WarpTaps { int x0, y0; float wx1, wy1; };
 // bilinear taps of output pixel (x, y) (grid_sample, zeros, align_corners=False; as warp_kernel)
@@ -727,9 +729,10 @@ __global__ __launch_bounds__(256) void wb_gather_kernel(int n, int h, int w, int
                                                         const int* __restrict__ counts, const int* __restrict__ offsets,
                                                         const int2* __restrict__ records, dbsr_tensor gate,
                                                         dbsr_tensor dfeat) {
+    __shared__ int2 sorted[4][64];
     const int hw = h * w;
-    const int lane = threadIdx.x & 63;
-    const long long q = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const long long q = (long long)blockIdx.x * 4 + wv;
     if (q >= (long long)n * hw) return;
     const int p = (int)(q / hw), rr = (int)(q - (long long)p * hw);
     const int cnt = counts[q];
@@ -737,19 +740,52 @@ __global__ __launch_bounds__(256) void wb_gather_kernel(int n, int h, int w, int
     const T* src = img_ptr<T>(dout, p);
     T* dst = img_ptr<T>(dfeat, p) + (long long)rr * dfeat.ld;
     const T* gp = gate.ptr ? img_ptr<T>(gate, p) + (long long)rr * gate.ld : nullptr;
+    if (cnt <= 64) {
+        // rank of each record by source pixel (lane e holds record e), then the records in that order in the LDS
+        const int2 mine = lane < cnt ? rec[lane] : int2{0x7fffffff, 0};
+        int rank = 0;
+        for (int j = 0; j < cnt; ++j) rank += __shfl(mine.x, j) < mine.x;
+        if (lane < cnt) sorted[wv][rank] = mine;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    // record e in source-pixel order: from the LDS, or (more than 64 contributions: strongly converging flows)
+    // the e-th smallest source found by a wave-wide minimum over the pixel's records
+    int last = -1;
+    auto record = [&](int e) -> int2 {
+        if (cnt <= 64) return sorted[wv][e];
+        int bx = 0x7fffffff, by = 0;
+        for (int i = lane; i < cnt; i += 64) {
+            const int2 r = rec[i];
+            if (r.x > last && r.x < bx) { bx = r.x; by = r.y; }
+        }
+        for (int o = 32; o >= 1; o >>= 1) {
+            const int ox = __shfl_xor(bx, o), oy = __shfl_xor(by, o);
+            if (ox < bx) { bx = ox; by = oy; }
+        }
+        last = bx;
+        return int2{bx, by};
+    };
     for (int c0 = 0; c0 < C; c0 += 512) {
         const int c = c0 + lane * 8;
-        if (c >= C) break;
+        const bool on = c < C;              // (lanes past C stay in the loop: record() may need the whole wave)
         float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        last = -1;
         for (int e0 = 0; e0 < cnt; e0 += 4) {
             float d[4][8];
             float wt[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 if (e0 + u < cnt) {
-                    const int2 r = rec[e0 + u];
+                    const int2 r = record(e0 + u);
                     wt[u] = __int_as_float(r.y);
-                    load8(src + (long long)r.x * dout.ld + c, d[u]);
+                    if (on) {
+                        load8(src + (long long)r.x * dout.ld + c, d[u]);
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) d[u][j] = 0.f;
+                    }
                 } else {
                     wt[u] = 0.f;
 #pragma unroll
@@ -761,6 +797,7 @@ __global__ __launch_bounds__(256) void wb_gather_kernel(int n, int h, int w, int
 #pragma unroll
                 for (int j = 0; j < 8; ++j) a[j] = fmaf(wt[u], d[u][j], a[j]);
         }
+        if (!on) continue;
         if (gp) {
             float g[8];
             load8(gp + c, g);

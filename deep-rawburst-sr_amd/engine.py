@@ -188,6 +188,7 @@ class Plan:
         self.streams = {}
         self.max_blocks = 0  # CU cap for lane-0 persistent convs issued while a side lane runs
         self.max_blocks_cap = 0
+        self.plan_rows = None  # (slab rows, whole-image rows): convs dispatch as on the whole image (plan_h)
 
     def add(self, name, fn, *args, work=None):
         if work is not None:
@@ -295,6 +296,10 @@ class Plan:
         d.workspace, d.workspace_bytes = None, 0
         d.precise = 1 if precise else 0
         d.max_blocks = self.max_blocks if self.lane == 0 else 0
+        if self.plan_rows is not None:
+            slab, full = self.plan_rows
+            if oh % slab == 0:
+                d.plan_h = full * (oh // slab)
         self.keep.append(d)
         return d
 
@@ -1017,16 +1022,13 @@ class DBSREngine:
             plan.valid = (0, H * self.s)
         else:
             lo, hi = rows
-            halo = self.decoder_halo()
-            y0, y1 = max(0, lo - halo), min(H, hi + halo)
-            # widen the slab to a multiple of 16 rows where the image allows (the trunk kernels' tile height;
-            # extra context leaves the valid rows exact)
-            while (y1 - y0) % 16 and (y0 > 0 or y1 < H):
-                if y0 > 0:
-                    y0 -= 1
-                else:
-                    y1 += 1
+            from .parallel import decoder_slab
+            y0, y1 = decoder_slab(lo, hi, H, self.decoder_halo())
+            # every conv takes the whole image's kernel, tile and K split (plan_h), so the slab's rows are
+            # bitwise the unsplit decoder's: kernel choice never depends on the slab height
+            plan.plan_rows = (y1 - y0, H)
             self._decoder(plan, B, y1 - y0, W, FUS.rows(y0, y1), bufs)
+            plan.plan_rows = None
             plan.valid = ((lo - y0) * self.s, (hi - y0) * self.s)
         plan.keep.append(FUS)
         plan.finalize_workspace(dev)

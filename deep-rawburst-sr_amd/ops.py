@@ -161,6 +161,7 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, act=L.ACT_NONE
                                          s), 'dbsr_conv2d_head')
         return out
     conv2d.last_kernel = L.lib().dbsr_conv_kernel_for(d)     # which kernel family ran (tests)
+    conv2d.last_variant = L.lib().dbsr_conv_dispatch_variant(d)
     L.check(L.lib().dbsr_conv2d(d, s), 'dbsr_conv2d')
     return y[..., :pc].permute(0, 3, 1, 2).contiguous()
 
@@ -228,6 +229,7 @@ def conv2d_dgrad(dy, weight, residual=None, gate=None, compute_dtype=torch.float
     need = L.lib().dbsr_conv_workspace_bytes(d)
     ws = torch.zeros(max(need // 4, 1), dtype=torch.float32, device=dy.device)
     d.workspace, d.workspace_bytes = ws.data_ptr(), need
+    conv2d_dgrad.last_kernel = L.lib().dbsr_conv_kernel_for(d)     # which kernel family ran (tests)
     L.check(L.lib().dbsr_conv2d(d, s), 'dbsr_conv2d (dgrad)')
     return y[..., :Cin].permute(0, 3, 1, 2).contiguous()
 

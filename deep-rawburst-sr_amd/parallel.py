@@ -86,6 +86,19 @@ def decoder_halo_rows(n_pre, n_post, s, blur=True):
     return n_lr + (n_hr + s - 1) // s
 
 
+def decoder_slab(lo, hi, total_rows, halo, align=16):
+    """LR rows [y0, y1) a rank decodes for its rows [lo, hi): widened by `halo` on each side, then to a multiple
+    of `align` rows where the image allows (the conv tiles' height; extra context leaves [lo, hi) exact).  Its
+    convs dispatch as on the whole image (dbsr_conv_desc.plan_h), which every multiple of 16 rows can tile."""
+    y0, y1 = max(0, lo - halo), min(total_rows, hi + halo)
+    while (y1 - y0) % align and (y0 > 0 or y1 < total_rows):
+        if y0 > 0:
+            y0 -= 1
+        else:
+            y1 += 1
+    return y0, y1
+
+
 def gather_rows(slab, total_rows, rows_per_lr=1):
     """All-gather per-rank row slabs [B, C, r_i, W] (rank r holds LR rows shard_range(total_rows, r, R), i.e.
     rows_per_lr times as many prediction rows) into [B, C, rows_per_lr * total_rows, W] in rank order."""

@@ -107,10 +107,15 @@ class DBSRTrainer:
             # subnormal, so an fp16 backward would underflow to zero
             raise ValueError('DBSRTrainer: train in torch.bfloat16 or torch.float32 (fp16 has no loss scaling here)')
         self.lr, self.betas, self.eps, self.bi = lr, betas, eps, boundary_ignore
+        if getattr(net.encoder, 'train_alignmentnet', False):
+            # the reference then backpropagates into PWC-Net (encoders.py:56-57); the HIP backward stops at the
+            # flows, so refuse rather than train without alignment gradients
+            raise NotImplementedError('DBSRTrainer: train_alignmentnet=True (PWC-Net training) is not on the HIP '
+                                      'backward; build the net with train_alignmentnet=False (dbsrnet_cvpr2021 default)')
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if (dist.is_available() and dist.is_initialized()) else 1
-        for p in net.encoder.alignment_net.parameters():
-            p.requires_grad_(False)                           # frozen PWC-Net (encoders.py:56-61)
+        # PWC-Net runs without gradients (train_alignmentnet=False: encoders.py:58-61); its parameters are left
+        # as the caller set them -- they never receive a .grad from this backward
         mods = self._trainable_convs()
         self.params = []
         for m in mods:
@@ -609,10 +614,21 @@ class _DBSRTrainForward(torch.autograd.Function):
         return (None, None) + tuple(ctx.engine.backward_from(ctx.token, gpred.contiguous()))
 
 
+def _aliased(eng):
+    """Every trained parameter still lives in the trainer's flat buffer (p.data = ..., load_state_dict(assign=True)
+    or a device move replace the storage; the trainer would then pack a stale copy)."""
+    cur = [p for m in trainable_convs(eng.net) for p in [m.weight] + ([m.bias] if m.bias is not None else [])]
+    if len(cur) != len(eng.params) or any(a is not b for a, b in zip(cur, eng.params)):
+        return False                                   # new Parameter objects (load_state_dict(assign=True))
+    base = eng.flat.data_ptr()
+    return all(p.data_ptr() == base + 4 * eng.offset[id(p)][0] and p.device == eng.dev and
+               p.dtype == torch.float32 for p in eng.params)
+
+
 def train_forward(net, burst):
     """pred, {'offsets', 'fusion_weights'} of DBSRNet.forward with autograd to the DBSR parameters."""
     eng = getattr(net, '_train_engine', None)
-    if eng is None or eng.net is not net or eng.dtype != net.compute_dtype:
+    if eng is None or eng.net is not net or eng.dtype != net.compute_dtype or not _aliased(eng):
         eng = net._train_engine = DBSRTrainer(net, optimizer=False)
     pred, offs, fw = _DBSRTrainForward.apply(burst, eng, *eng.params)
     from .engine import DBSRAux

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define DBSR_ABI_VERSION 12
+#define DBSR_ABI_VERSION 13
 
 enum { DBSR_F32 = 0, DBSR_BF16 = 1, DBSR_F16 = 2 };
 enum { DBSR_ACT_NONE = 0, DBSR_ACT_RELU = 1, DBSR_ACT_LRELU = 2 };      /* LeakyReLU slope 0.1 */
@@ -88,6 +88,12 @@ typedef struct dbsr_conv_desc {
     dbsr_tensor gate;                 /* gate.ptr != NULL: out = (gate > 0) ? out : 0 after the residual --
                                          the ReLU backward of the layer that produced the conv's input
                                          (training dgrad); NHWC, output dtype; not with shuffle/NCHW out */
+    int plan_h;                       /* > 0: choose the kernel, tile and K split as for an image plan_h output
+                                         rows tall (0 = out_h).  A frame-sharded rank decodes a row slab of the
+                                         whole image (decoders.py:54-62 run on all rows by the reference); with
+                                         plan_h = the whole image's rows the slab takes exactly the whole-image
+                                         plan's kernels, so its rows are bitwise the unsplit ones.  The slab's
+                                         out_h must suit the chosen tile (multiples of 16 always do) */
 } dbsr_conv_desc;
 
 /* Packed weight layout: [cout_pad][kgp*8] with k-group kg = (ky*kw+kx)*(cinp/8) + c/8, where
@@ -115,6 +121,11 @@ int dbsr_set_conv_algo(int algo);
  * 3 PixelShuffle upsampler (bf16 1x1 with DBSR_OUT_SHUFFLE, 32 channels per sub-pixel), 2 pipelined,
  * 6 narrow-output 3x3 (16-bit, cout <= 4, cin >= 256, pad 1: the PWC level-2 flow head), 1 LDS-tiled, 0 generic. */
 int dbsr_conv_kernel_for(const dbsr_conv_desc* d);
+/* The full dispatch decision for `d`: kernel_for * 1000000 + the variant (weight-stationary: tile width*100 +
+ * height; pipelined: tile config; LDS-tiled: cout tile*1000 + pixel tile; generic: cout tile*10000 + pixel
+ * tile*1000 + K split; precise: pixel tile).  Two descs with equal variants sum every output in the same
+ * order (the frame-sharding tests compare a slab's variants with the whole image's). */
+int dbsr_conv_dispatch_variant(const dbsr_conv_desc* d);
 /* A 32-channel ResBlock conv2 fused with a 1x1 head (the decoder's last post-ResBlock + RGB predictor,
  * decoders.py:59-61 / blocks.py:94-96): t = ReLU(conv(x) + bias + residual) stays in registers (d->y is
  * not written) and out = ReLU(head_w . t + head_b) is stored fp32 NCHW (head_out.img_stride =

@@ -177,3 +177,74 @@ def test_lds_dma_kernels_own_their_simds():
     rows, bad = mod.audit(os.path.join(repo, 'deep-rawburst-sr_amd', 'libdbsr_hip.so'))
     assert len(rows) >= 40, 'expected the pipelined / weight-stationary / tiled LDS-DMA kernels'
     assert not bad, bad
+
+
+def _cfg4_decoder_descs(L, rows, full=96, W=96, s=16):
+    """ConvDescs of configs[4]'s decoder (fp16, x16; decoders.py:54-62 with default_synthetic's widths) on `rows`
+    LR rows of a `full`-row image: (name, desc) in launch order (host logic only, fake pointers)."""
+    fm = L.FrameMap(1, 1, 0, 1)
+
+    def desc(cin, cout, k, h, w, ldx, ldy, res=False, act=L.ACT_RELU, post=L.ACT_NONE, out_mode=L.OUT_NHWC,
+             shuffle=0, precise=0, scale=1):
+        d = L.ConvDesc()
+        d.n_frames = 1
+        d.x = L.Tensor(1, L.DBSR_F16, h * w * ldx, ldx, 0, fm)
+        d.in_h, d.in_w, d.cin = h, w, cin
+        d.w = 1
+        d.cout, d.kh, d.kw, d.stride, d.pad, d.dil = cout, k, k, 1, k // 2, 1
+        yd = L.DBSR_F32 if out_mode == L.OUT_NCHW_F32 else L.DBSR_F16
+        d.y = L.Tensor(1, yd, h * w * ldy, ldy, 0, fm)
+        d.out_h, d.out_w = h, w
+        d.act, d.post_act = act, post
+        d.res = L.Tensor(1, L.DBSR_F16, h * w * ldy, ldy, 0, fm) if res else L.NULL_TENSOR
+        d.out_mode, d.shuffle, d.precise = out_mode, shuffle, precise
+        if rows != full:
+            d.plan_h = full * scale
+        return d
+    out = [('dec.init', desc(512, 64, 3, rows, W, 512, 64))]
+    for i in range(5):
+        out.append(('dec.pre%d.conv1' % i, desc(64, 64, 3, rows, W, 64, 64)))
+        out.append(('dec.pre%d.conv2' % i, desc(64, 64, 3, rows, W, 64, 64, res=True, act=L.ACT_NONE,
+                                                post=L.ACT_RELU)))
+    out.append(('dec.upsample', desc(64, 32 * s * s, 1, rows, W, 64, 32, out_mode=L.OUT_SHUFFLE, shuffle=s)))
+    for i in range(4):
+        out.append(('dec.post%d.conv1' % i, desc(32, 32, 3, rows * s, W * s, 32, 32, scale=s)))
+        out.append(('dec.post%d.conv2' % i, desc(32, 32, 3, rows * s, W * s, 32, 32, res=True, act=L.ACT_NONE,
+                                                 post=L.ACT_RELU, scale=s)))
+    out.append(('dec.predictor', desc(32, 3, 1, rows * s, W * s, 32, 1, out_mode=L.OUT_NCHW_F32, precise=1, scale=s)))
+    return out
+
+
+def test_frame_shard_slabs_dispatch_as_whole(L):
+    """a frame-sharded rank's decoder slab (configs[4]: 4 ranks, 96x96 LR -> x16) takes, conv for
+    conv, the whole image's kernel, tile and K split (dbsr_conv_dispatch_variant, with plan_h), so its rows of the
+    prediction are bitwise the unsplit decoder's; without plan_h the 48-row slabs took other kernels (the
+    round-3 regression: 16x8 weight-stationary tiles on the whole image, another kernel on the slabs)."""
+    from dbsr_amd.parallel import decoder_halo_rows, decoder_slab, shard_range
+    lib = L.lib()
+    whole = [(n, lib.dbsr_conv_dispatch_variant(d), lib.dbsr_conv_head_ok(d)) for n, d in _cfg4_decoder_descs(L, 96)]
+    assert all(v >= 0 for _, v, _ in whole)
+    halo = decoder_halo_rows(5, 4, 16, True)
+    unpinned_differs = False
+    for r in range(4):
+        y0, y1 = decoder_slab(*shard_range(96, r, 4), 96, halo)
+        assert (y1 - y0) % 16 == 0
+        slab = [(n, lib.dbsr_conv_dispatch_variant(d), lib.dbsr_conv_head_ok(d))
+                for n, d in _cfg4_decoder_descs(L, y1 - y0)]
+        assert slab == whole, (r, [(a, b) for a, b in zip(slab, whole) if a != b])
+        for n, d in _cfg4_decoder_descs(L, y1 - y0):
+            d.plan_h = 0
+            unpinned_differs |= lib.dbsr_conv_dispatch_variant(d) != dict((a, b) for a, b, _ in whole)[n]
+    assert unpinned_differs, 'the slab geometry alone no longer changes any dispatch: the test lost its teeth'
+
+
+def test_plan_h_misfit_rejected(L):
+    """A slab whose height cannot take the tile chosen for plan_h fails loudly instead of falling back to
+    another kernel (which would change the summation order)."""
+    lib = L.lib()
+    d = dict(_cfg4_decoder_descs(L, 36))['dec.pre0.conv1']     # 36 rows: not a multiple of the 8-row tile
+    d.plan_h = 96                                                # whole image: 16x8 weight-stationary tiles
+    assert lib.dbsr_conv_kernel_for(d) == 4
+    d.x.ptr, d.y.ptr = 16, 16
+    assert lib.dbsr_conv2d(d, None) == -1
+    assert b'plan_h' in lib.dbsr_last_error()
