@@ -66,6 +66,10 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     ap.add_argument('--kernel-breakdown', action='store_true', help='print per-op device times to stderr')
+    ap.add_argument('--conv-algo', type=int, default=None,
+                    help='diagnostic A/B: dbsr_set_conv_algo value (include/dbsr_hip.h); default: the library default')
+    ap.add_argument('--no-op-timing', action='store_true',
+                    help='skip the per-op timing passes after the timed region (profiling runs: only graph replays)')
     ap.add_argument('--zero-flow', action='store_true', help='diagnostic: identity-flow stub instead of PWC-Net')
     ap.add_argument('--mode', default='infer', choices=['infer', 'train'],
                     help='train: configs[3] training step (defaults 128x128, batch 8 per GPU, RCCL grad all-reduce)')
@@ -231,6 +235,9 @@ def cpu_baseline(N, H, W, seconds):
                 break
     return {'value': n / el, 'unit': 'bursts/s', 'cores': torch.get_num_threads(), 'kind': 'port',
             'cpu_model': cpu_model(), 'host_cpus': os.cpu_count(),
+            'cores_note': 'torch intra-op threads = OMP_NUM_THREADS (%s): the GPU box allots 16 CPUs per GPU of its '
+                          '%d host CPUs, so the baseline runs on that share, not on all of them'
+                          % (os.environ.get('OMP_NUM_THREADS', 'unset'), os.cpu_count()),
             'sample': f'{n} batch-1 bursts of {N}x{H}x{W} (fp32 oracle/dbsr_oracle.py, {el:.1f} s)'}
 
 
@@ -263,6 +270,9 @@ def main():
     from dbsr_amd.burst import synthetic_bursts
     from dbsr_amd.parallel import shard_range
     dtype = getattr(torch, DTYPES[args.dtype])
+    if args.conv_algo is not None:
+        from dbsr_amd import _lib
+        _lib.check(_lib.lib().dbsr_set_conv_algo(args.conv_algo), 'dbsr_set_conv_algo')
     net = dbsr_amd.build_synthetic_net(seed=0).to(dev).eval()
     net.set_compute_dtype(dtype)
     net.use_graph = not args.no_graph
@@ -290,66 +300,95 @@ def main():
             el = max_over_ranks(el, device=dev)
             td.barrier()
 
-        # ---- per-kernel device times (HIP events on the plan's stream), outside the timed region ----
+        # ---- per-kernel device times (HIP events), outside the timed region: inside the step as the step runs
+        # them (lanes concurrent, lane-0 convs capped while PWC-Net runs), and each op alone on the whole chip ----
         eng = net._engine
         plan = eng.plans[(B, N, S, S)]
-        times = plan.time_ops(torch.cuda.current_stream(dev).cuda_stream, reps=10)
+        times, times_chip = None, None
+        if not args.no_op_timing:
+            cur = torch.cuda.current_stream(dev).cuda_stream
+            times = plan.time_ops_in_step(cur, reps=5)
+            times_chip = plan.time_ops(cur, reps=10)
 
     ms_step = el / args.steps * 1e3
     value = world * B * args.steps / el
-    fam = {}
-    for i, (name, ms) in enumerate(times):
-        if name.startswith('sync.'):
-            continue
-        kind = plan.kernel.get(i) or name.split('.')[-1]
-        f = fam.setdefault(kind, [0.0, 0.0, 0])
-        f[0] += ms
-        f[1] += plan.work[i][1] if i in plan.work else 0.0
-        f[2] += 1
     is_conv = lambda k: k in CONV_FAMILIES                  # noqa: E731
-    conv_flop = sum(w for kind, (ms, w, n) in fam.items() if is_conv(kind))
     peak_t = PEAK_MFMA_TFLOPS[args.dtype]
     traffic = load_traffic() if args.dtype != 'fp32' else {}
-    # the dominant kernel family (most device time per forward)
-    dom = max((k for k in fam if is_conv(k)), key=lambda k: fam[k][0])
-    t_ms, t_flop, t_n = fam[dom]
-    t_tf = t_flop / (t_ms * 1e-3) / 1e12
-    roof = {'bound': 'mfma', 'kernel': KERNEL_DESC[dom] + ', %d launches per forward; achieved = their algorithmic '
-                                                         'FLOPs / their summed event-timed durations)' % t_n,
-            'achieved': round(t_tf, 2), 'peak': peak_t, 'unit': 'TFLOP/s', 'frac': round(t_tf / peak_t, 4),
-            'traffic': traffic.get(dom, {}).get('bytes_per_launch'),
-            'traffic_source': traffic.get(dom, {}).get('source'),
-            'timing': 'each op re-launched 10x between HIP events on the plan stream after the timed region, on the '
-                      'whole chip (inside the step the encoder convs are capped to %d of %d CUs while PWC-Net runs '
-                      'on the side lane)' % (plan.max_blocks_cap, torch.cuda.get_device_properties(dev).multi_processor_count)}
-    # every conv family against the same dense peak (the roofline object above is the dominant one)
-    fam_roof = {k: {'achieved_tflops': round(w / (ms * 1e-3) / 1e12, 2), 'frac': round(w / (ms * 1e-3) / 1e12 / peak_t, 4),
-                    'ms': round(ms, 4), 'launches': n, 'traffic': traffic.get(k, {}).get('bytes_per_launch')}
-                for k, (ms, w, n) in fam.items() if is_conv(k) and ms > 0}
-    conv_ms = sum(ms for kind, (ms, w, n) in fam.items() if is_conv(kind))
-    conv_n = sum(n for kind, (ms, w, n) in fam.items() if is_conv(kind))
-    all_conv_tf = conv_flop / (conv_ms * 1e-3) / 1e12
-    hbm = {}
-    for k in ('warp', 'fuse'):
-        if k in fam:
-            ms, by, n = fam[k]
-            gbs = by / (ms * 1e-3) / 1e9
-            hbm[k] = {'bound': 'hbm', 'achieved': round(gbs, 1), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
-                      'frac': round(gbs / PEAK_HBM_GBS, 4), 'traffic': traffic.get(k, {}).get('bytes_per_launch'),
-                      'us': round(ms * 1e3, 2), 'alg_bytes': by / n}
-    if args.kernel_breakdown and rank == 0:
-        for i, (name, ms) in enumerate(times):
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+
+    def families(tt):
+        fam = {}
+        for i, (name, ms) in enumerate(tt):
             if name.startswith('sync.'):
                 continue
-            kind = plan.kernel.get(i) or '-'
-            w = plan.work[i][1] if i in plan.work else 0.0
-            rate = '%8.1f %s' % ((w / (ms * 1e-3) / 1e12, 'TF/s') if is_conv(kind) else
-                                 (w / (ms * 1e-3) / 1e9, 'GB/s')) if (w and ms) else ''
-            print(f'{name:32s} {ms * 1e3:9.1f} us  {kind:15s} {rate}', file=sys.stderr)
-        for k, (ms, w, n) in sorted(fam.items(), key=lambda kv: -kv[1][0]):
-            print(f'[family] {k:12s} {ms * 1e3:9.1f} us  n={n}', file=sys.stderr)
-        print(f'sum of op times {sum(t for _, t in times) * 1e3:.1f} us vs step {ms_step * 1e3:.1f} us',
-              file=sys.stderr)
+            kind = plan.kernel.get(i) or name.split('.')[-1]
+            f = fam.setdefault(kind, [0.0, 0.0, 0])
+            f[0] += ms
+            f[1] += plan.work[i][1] if i in plan.work else 0.0
+            f[2] += 1
+        return fam
+
+    def conv_roofline(fam, dom, timing):
+        t_ms, t_flop, t_n = fam[dom]
+        t_tf = t_flop / (t_ms * 1e-3) / 1e12
+        return {'bound': 'mfma', 'kernel': KERNEL_DESC[dom] + ', %d launches per forward; achieved = their '
+                'algorithmic FLOPs / their summed event-timed durations)' % t_n,
+                'achieved': round(t_tf, 2), 'peak': peak_t, 'unit': 'TFLOP/s', 'frac': round(t_tf / peak_t, 4),
+                'traffic': traffic.get(dom, {}).get('bytes_per_launch'),
+                'traffic_source': traffic.get(dom, {}).get('source'), 'timing': timing}
+
+    def fam_rooflines(fam):
+        return {k: {'achieved_tflops': round(w / (ms * 1e-3) / 1e12, 2), 'frac': round(w / (ms * 1e-3) / 1e12 / peak_t, 4),
+                    'ms': round(ms, 4), 'launches': n, 'traffic': traffic.get(k, {}).get('bytes_per_launch')}
+                for k, (ms, w, n) in fam.items() if is_conv(k) and ms > 0}
+
+    roof = roof_chip = fam_roof = fam_roof_chip = hbm = conv_all = None
+    conv_flop = None
+    if times is not None:
+        fam, fam_chip = families(times), families(times_chip)
+        conv_flop = sum(w for kind, (ms, w, n) in fam.items() if is_conv(kind))
+        # the dominant kernel family: the most device time per forward INSIDE the step
+        dom = max((k for k in fam if is_conv(k)), key=lambda k: fam[k][0])
+        roof = conv_roofline(fam, dom, 'in-step: each op of 5 eagerly issued forwards bracketed by HIP events on '
+                             'the stream it runs on, lanes concurrent as in the step (lane-0 convs capped to %d of %d '
+                             'CUs while PWC-Net runs on the side lane), the forward queued behind a spin kernel so no '
+                             'host gap falls inside an op' % (plan.max_blocks_cap, ncu))
+        dom_chip = max((k for k in fam_chip if is_conv(k)), key=lambda k: fam_chip[k][0])
+        roof_chip = conv_roofline(fam_chip, dom_chip, 'whole chip: each op re-launched 10x alone between HIP events '
+                                  'on the plan stream, uncapped')
+        fam_roof, fam_roof_chip = fam_rooflines(fam), fam_rooflines(fam_chip)
+        conv_ms = sum(ms for kind, (ms, w, n) in fam_chip.items() if is_conv(kind))
+        conv_n = sum(n for kind, (ms, w, n) in fam_chip.items() if is_conv(kind))
+        conv_all = {'achieved_tflops_whole_chip': round(conv_flop / (conv_ms * 1e-3) / 1e12, 2), 'launches': conv_n,
+                    'step_frac': round(conv_flop / (ms_step * 1e-3) / 1e12 / peak_t, 4),
+                    'ms_by_kernel_in_step': {k: round(v[0], 3) for k, v in fam.items() if is_conv(k)},
+                    'ms_by_kernel_whole_chip': {k: round(v[0], 3) for k, v in fam_chip.items() if is_conv(k)}}
+        hbm = {}
+        for k in ('warp', 'fuse'):
+            if k in fam_chip:
+                ms, by, n = fam_chip[k]
+                gbs = by / (ms * 1e-3) / 1e9
+                ms_in = fam[k][0]
+                hbm[k] = {'bound': 'hbm', 'achieved': round(gbs, 1), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
+                          'frac': round(gbs / PEAK_HBM_GBS, 4), 'traffic': traffic.get(k, {}).get('bytes_per_launch'),
+                          'us': round(ms * 1e3, 2), 'alg_bytes': by / n,
+                          'frac_in_step': round(by / (ms_in * 1e-3) / 1e9 / PEAK_HBM_GBS, 4), 'us_in_step': round(ms_in * 1e3, 2)}
+        if args.kernel_breakdown and rank == 0:
+            for i, ((name, ms), (_, msc)) in enumerate(zip(times, times_chip)):
+                if name.startswith('sync.'):
+                    continue
+                kind = plan.kernel.get(i) or '-'
+                w = plan.work[i][1] if i in plan.work else 0.0
+                rate = '%8.1f %s' % ((w / (msc * 1e-3) / 1e12, 'TF/s') if is_conv(kind) else
+                                     (w / (msc * 1e-3) / 1e9, 'GB/s')) if (w and msc) else ''
+                print(f'{name:32s} in-step {ms * 1e3:8.1f} us  chip {msc * 1e3:8.1f} us  {kind:15s} {rate}',
+                      file=sys.stderr)
+            for k, (ms, w, n) in sorted(fam.items(), key=lambda kv: -kv[1][0]):
+                print(f'[family] {k:12s} in-step {ms * 1e3:9.1f} us  chip {fam_chip[k][0] * 1e3:9.1f} us  n={n}',
+                      file=sys.stderr)
+            print(f'sum of op times in-step {sum(t for _, t in times) * 1e3:.1f} us (lanes overlap), whole chip '
+                  f'{sum(t for _, t in times_chip) * 1e3:.1f} us vs step {ms_step * 1e3:.1f} us', file=sys.stderr)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -366,10 +405,9 @@ def main():
                        'global_batch': B * world, 'frames': N, 'height': S, 'width': S, 'out_size': S * 8,
                        'parallelism': 'dp%d (independent bursts per rank)' % world,
                        'hip_graph': not args.no_graph, 'fusion_weights_written': True},
-            'roofline': roof, 'roofline_hbm': hbm,
-            'roofline_families': fam_roof,
-            'conv_all': {'achieved_tflops': round(all_conv_tf, 2), 'launches': conv_n,
-                         'ms_by_kernel': {k: round(v[0], 3) for k, v in fam.items() if is_conv(k)}},
+            'roofline': roof, 'roofline_whole_chip': roof_chip, 'roofline_hbm': hbm,
+            'roofline_families': fam_roof, 'roofline_families_whole_chip': fam_roof_chip,
+            'conv_all': conv_all,
             'cpu_baseline': cpu,
             'conv_flop_per_step': conv_flop,
         }

@@ -24,6 +24,25 @@ typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
 // kernel that does not claim its SIMDs.  Costs nothing at 2 waves per SIMD (their occupancy is already 2).
 #define DBSR_OWN_SIMDS() asm volatile("" ::: "v255")
 
+// Barrier after LDS-DMA (buffer/global_load ... lds): every wave first drains its own vector-memory queue, so
+// the pieces it DMA'd have landed before any wave reads them.  __syncthreads() alone does not guarantee this:
+// its workgroup fence needs no vmcnt(0), and the s_waitcnt the compiler puts before a barrier is sized for
+// the LDS reads of THIS wave that it can see alias the DMA (tools/isa_audit.py checks every barrier).
+// The wait is the s_waitcnt builtin rather than inline asm so that the compiler's own wait insertion knows
+// the queue is empty afterwards (it does not read inline asm) and emits no conservative waits later on.
+__device__ __forceinline__ void vm_drain() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(0x0F70);           // vmcnt(0), expcnt / lgkmcnt unconstrained (gfx9 encoding)
+    asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ void dma_barrier() {
+    vm_drain();
+    __syncthreads();
+}
+// s_waitcnt vmcnt(n), n < 64 (gfx9 encoding: vmcnt bits [3:0] and [15:14])
+#define DBSR_VM_WAIT(n) do { asm volatile("" ::: "memory"); \
+    __builtin_amdgcn_s_waitcnt(0x0F70 | ((n) & 15) | (((n) >> 4) << 14)); asm volatile("" ::: "memory"); } while (0)
+
 __device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((unsigned)v) << 16); }
 
 // fp32 -> bf16, round-to-nearest-even, NaN kept NaN: the plain cast lowers to the hardware

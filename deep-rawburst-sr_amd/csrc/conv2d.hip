@@ -19,6 +19,7 @@
 #include "common.hpp"
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 
 using namespace dbsr;
@@ -671,7 +672,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_tiled_kernel(ConvK k, int tile
 
     for (int chunk = 0; chunk < nchunks; ++chunk) {
         issue(chunk);
-        __syncthreads();                 // vmcnt(0) for the LDS-DMA + barrier
+        dma_barrier();                   // vmcnt(0) for the LDS-DMA + barrier
         // taps software-pipelined through two fragment sets: tap t+1's ds_reads are in flight during
         // tap t's MFMAs
         Frag<T> a0[WM / 16], b0[WN / 16], a1[WM / 16], b1[WN / 16];
@@ -1104,11 +1105,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pipe_kernel(ConvK k, int tiles
     for (int ti = 0; ti < my_tiles; ++ti) {
         for (int c = 0; c < nchunks; ++c, ++s) {
             PIPE_STAMP(2 + s * 5);
-#ifdef DBSR_PIPE_STAMPS
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             PIPE_STAMP(3 + s * 5);
-#endif
-            __syncthreads();            // stage s landed (vmcnt(0) + barrier); stage s-1 fully consumed
+            dma_barrier();              // stage s landed (vmcnt(0) + barrier); stage s-1 fully consumed
             PIPE_STAMP(4 + s * 5);
             const bool fin = c == 0 && ti > 0;
             if (fin) epilogue(prev);
@@ -1183,7 +1181,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pipe_kernel(ConvK k, int tiles
             }
         }
     }
-    __syncthreads();                    // the last tile's residual landed (vmcnt(0))
+    dma_barrier();                      // the last tile's residual loads landed
     epilogue(prev);
 #pragma unroll
     for (int q = 0; q < C::NOUT; ++q) store_piece(q, prev);
@@ -1499,8 +1497,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ws_kernel(ConvK k, int tiles_x
     for (int it = 0; it < C::PER; ++it) dma(it, cur, 0);
     // the wave's A-fragments of both 16-cout blocks for every (chunk, tap), from the staged weights; the
     // loop's first barrier then orders these reads before any wave's DMA into the staging region
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    dma_barrier();
     Frag<T> wr[NCH][9][2];
 #pragma unroll
     for (int c = 0; c < NCH; ++c)
@@ -1514,11 +1511,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ws_kernel(ConvK k, int tiles_x
     PIPE_STAMP(2);
     for (int ti = 0; ti < my_tiles; ++ti) {
         PIPE_STAMP(3 + ti * 5);
-#ifdef DBSR_PIPE_STAMPS
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        vm_drain();                     // this wave's LDS-DMAs landed, then the barrier: everyone's did
         PIPE_STAMP(4 + ti * 5);
-#endif
-        __syncthreads();                // this tile's halo landed (vmcnt(0) + barrier); the other buffer is free
+        __syncthreads();                // this tile's halo landed; the other buffer is free
         PIPE_STAMP(5 + ti * 5);
         const bool more = ti + 1 < my_tiles;
         if (ti > 0) store(prev);        // previous tile's outputs (computed before the barrier)
@@ -1574,8 +1569,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ws_kernel(ConvK k, int tiles_x
         // ti + 2's residual, issued after the next barrier
         if constexpr (RES_BUFS > 0) {
             if (has_res && ti == 0) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __syncthreads();
+                dma_barrier();
             }
         }
         epilogue(cur, ti & 1);

@@ -140,21 +140,30 @@ class DBSRAux(dict):
 
 
 class PackedConv:
-    """One nn.Conv2d packed for dbsr_conv2d."""
-    def __init__(self, conv, dtype, device, stream, shuffle=1):
-        w = conv.weight.detach().to(device=device, dtype=torch.float32).contiguous()
-        b = conv.bias.detach().to(device=device, dtype=torch.float32).contiguous() if conv.bias is not None else None
+    """One nn.Conv2d packed for dbsr_conv2d.  recipe() -> (weight, bias | None) gives the source tensors
+    (default: the module's own); repack() re-packs them into the same buffers, so plans and captured graphs
+    that point at them stay valid."""
+    def __init__(self, conv, dtype, device, stream, shuffle=1, recipe=None):
+        self.recipe = recipe or (lambda: (conv.weight, conv.bias))
+        self.dtype, self.device, self.shuffle = dtype, device, shuffle
+        w, b = self.recipe()
         self.cout, self.cin, self.kh, self.kw = w.shape
         self.stride, self.pad, self.dil = conv.stride[0], conv.padding[0], conv.dilation[0]
         n = L.lib().dbsr_conv_packed_elems(self.cout, self.cin, self.kh, self.kw)
         self.w = torch.empty(n, dtype=dtype, device=device)
         self.bias = torch.empty(self.cout, dtype=torch.float32, device=device) if b is not None else None
+        self.repack(stream)
+
+    def repack(self, stream):
+        w, b = self.recipe()
+        w = w.detach().to(device=self.device, dtype=torch.float32).contiguous()
+        b = b.detach().to(device=self.device, dtype=torch.float32).contiguous() if b is not None else None
         L.check(L.lib().dbsr_conv_pack_weights(w.data_ptr(), b.data_ptr() if b is not None else None, self.cout,
-                                               self.cin, self.kh, self.kw, L.dtype_code(dtype), shuffle,
+                                               self.cin, self.kh, self.kw, L.dtype_code(self.dtype), self.shuffle,
                                                self.w.data_ptr(),
                                                self.bias.data_ptr() if self.bias is not None else None, stream),
                 'dbsr_conv_pack_weights')
-        self._keep = (w, b)
+        self._keep = (w, b)             # (the launch reads them asynchronously)
 
     def out_hw(self, h, w):
         return ((h + 2 * self.pad - self.dil * (self.kh - 1) - 1) // self.stride + 1,
@@ -356,6 +365,43 @@ class Plan:
             for d, mb in capped:
                 d.max_blocks = mb
 
+    def time_ops_in_step(self, stream, reps=3, hold_cycles=40_000_000):
+        """Average device time (ms) of each op inside a forward run the way the step runs it: every lane on its
+        own stream, the side lane concurrent with lane 0 and the lane-0 convs capped while it runs.  Each op is
+        bracketed by HIP events on the stream it runs on; the whole forward is queued behind a spin kernel
+        (`hold_cycles`) first, so host launch gaps never fall inside an op's events.  Unlike time_ops, the
+        durations include the sharing of the chip between the lanes (they overlap: their sum exceeds the step)."""
+        main = torch.cuda.current_stream()
+        assert main.cuda_stream == stream, 'time_ops_in_step: lanes fork from the current stream'
+        tot = [0.0] * len(self.ops)
+        for _ in range(reps):
+            torch.cuda._sleep(hold_cycles)
+            evs = []
+            for fn, args, name, lane in self.ops:
+                if fn is Plan.FORK:
+                    args[0].record(main)
+                    self.streams[lane].wait_event(args[0])
+                    evs.append(None)
+                    continue
+                if fn is Plan.JOIN:
+                    args[0].record(self.streams[lane])
+                    main.wait_event(args[0])
+                    evs.append(None)
+                    continue
+                st = main if lane == 0 else self.streams[lane]
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(st)
+                rc = fn(*args, stream if lane == 0 else st.cuda_stream)
+                if rc != 0:
+                    L.check(rc, name)
+                e1.record(st)
+                evs.append((e0, e1))
+            torch.cuda.synchronize()
+            for i, ev in enumerate(evs):
+                if ev is not None:
+                    tot[i] += ev[0].elapsed_time(ev[1])
+        return [(name, t / reps) for (fn, args, name, lane), t in zip(self.ops, tot)]
+
     def _time_ops(self, stream, reps):
         out = []
         for fn, args, name, lane in self.ops:
@@ -378,8 +424,8 @@ class _Weights:
     def __init__(self, dtype, device, stream):
         self.dtype, self.device, self.stream = dtype, device, stream
 
-    def conv(self, module, shuffle=1):
-        return PackedConv(module, self.dtype, self.device, self.stream, shuffle=shuffle)
+    def conv(self, module, shuffle=1, recipe=None):
+        return PackedConv(module, self.dtype, self.device, self.stream, shuffle=shuffle, recipe=recipe)
 
 
 def _param_signature(module):
@@ -580,6 +626,7 @@ class DBSREngine:
         self.plans = {}
         self.slots = {}
         self.graphs = {}
+        self.weights_stale = False
 
     def matches(self, net):
         return (net is self.net and self.dtype == net.compute_dtype and self.sig == _param_signature(net)
@@ -607,12 +654,11 @@ class DBSREngine:
         pd = mer.feat_project_layer[0].out_channels
         self.wp_split = None
         if DBSREngine.LINEAR_SPLIT and getattr(mer, 'use_base_frame', False) and pd % 32 == 0:
-            w0 = wp[0][0].weight.detach().float()
-            rest = types.SimpleNamespace(weight=w0[:, pd:].contiguous(), bias=wp[0][0].bias, stride=(1,),
-                                         padding=wp[0][0].padding, dilation=wp[0][0].dilation)
-            base = types.SimpleNamespace(weight=(w0[:, :pd] - w0[:, pd:2 * pd]).contiguous(), bias=None,
-                                         stride=(1,), padding=wp[0][0].padding, dilation=wp[0][0].dilation)
-            self.wp_split = (W.conv(rest), W.conv(base))
+            c0 = wp[0][0]
+            geo = types.SimpleNamespace(stride=(1,), padding=c0.padding, dilation=c0.dilation)
+            rest = lambda: (c0.weight.detach().float()[:, pd:], c0.bias)                               # noqa: E731
+            base = lambda: (c0.weight.detach().float()[:, :pd] - c0.weight.detach().float()[:, pd:2 * pd], None)  # noqa: E731
+            self.wp_split = (W.conv(geo, recipe=rest), W.conv(geo, recipe=base))
         self.wp_res = [(W.conv(b.conv1[0]), W.conv(b.conv2[0])) for b in wp[1:-1]]
         self.wp_out = W.conv(wp[-1][0])
         self.dec_init = W.conv(dec.init_layer[0])
@@ -634,6 +680,27 @@ class DBSREngine:
         self.device = device
         self.sig = _param_signature(net)
         self.plans, self.slots, self.graphs = {}, {}, {}
+        self.weights_stale = False
+
+    def refresh_weights(self):
+        """Re-pack the DBSR (non-PWC) weights in place after an optimizer updated the parameters through their
+        storage (DBSRTrainer.step's Adam kernel: no version bump, no new storage): plans and captured graphs
+        keep pointing at the same packed buffers.  PWC-Net is frozen in training (encoders.py:56-61)."""
+        stream = L.stream_ptr(self.device)
+        convs = [self.enc_init, self.enc_out, self.proj, self.ofe_init, self.wp_init, self.wp_out, self.dec_init,
+                 self.dec_up, self.pred]
+        for lst in (self.enc_res, self.ofe_res, self.wp_res, self.dec_pre, self.dec_post):
+            for c1, c2 in lst:
+                convs += [c1, c2]
+        if self.wp_split is not None:
+            convs += list(self.wp_split)
+        for pc in convs:
+            pc.repack(stream)
+        pm = self.net.decoder.predictor[0]
+        self.head_w.copy_(pm.weight.detach().reshape(pm.out_channels, -1))
+        if self.head_b is not None:
+            self.head_b.copy_(pm.bias.detach())
+        self.weights_stale = False
 
     def _resblocks(self, plan, name, blocks, n, hw, bufs, x_idx, dtype, head=None):
         """ResBlock chain (blocks.py:81-96) over ping-pong buffers; returns index of the result buffer
@@ -959,6 +1026,8 @@ class DBSREngine:
         dev = burst.device
         if self.device != dev or self.sig != _param_signature(self.net):
             self._pack(dev)
+        elif self.weights_stale:
+            self.refresh_weights()
         key = (B, N, H, W)
         if key not in self.slots:
             self._new_slot(key)
@@ -1040,6 +1109,8 @@ class DBSREngine:
             raise RuntimeError('DBSRNet (MI355X engine) needs the burst on a HIP device; got %s' % burst.device)
         if self.device != burst.device or self.sig != _param_signature(self.net):
             self._pack(burst.device)
+        elif self.weights_stale:
+            self.refresh_weights()
 
     def forward_partial(self, burst, first_frame):
         """Encoder, alignment, warp and weight predictor of a frame shard `burst` [B,n,4,H,W] (frame 0 =

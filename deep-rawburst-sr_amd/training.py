@@ -487,8 +487,11 @@ class DBSRTrainer:
         L.check(L.lib().dbsr_adam_step(self.n_params, self.flat.data_ptr(), self.flat_grad.data_ptr(),
                                        self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(), self.lr, self.betas[0],
                                        self.betas[1], self.eps, self.step_count, 1.0 / self.world, stream), 'adam')
-        # the inference engine packs from the module parameters (now updated in place): repack next forward
-        self.net._engine = None
+        # the inference engine packs from the module parameters (now updated in place through their storage):
+        # it re-packs them into its existing buffers at its next forward, keeping its plans and graphs
+        eng = getattr(self.net, '_engine', None)
+        if eng is not None:
+            eng.weights_stale = True
         return self.loss.clone()          # (self.loss is the plan's buffer, overwritten by the next step)
 
     def forward_backward(self, burst, frame_gt):

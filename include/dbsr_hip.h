@@ -114,7 +114,7 @@ int dbsr_conv2d(const dbsr_conv_desc* d, void* stream);
  * 48 or 64, height a multiple of 8, >= 256 tiles), else the two-barrier LDS-tiled 3x3 kernel where it
  * applies (3x3, stride 1, pad == dilation in {1,2,4,8}, cin > 16, out >= 8x8, NHWC out), else the
  * generic implicit-GEMM kernel; 1 = no pipelined kernel; 0 = generic kernel only; 3 = as 2 but the
- * pipelined kernel at any tile count (tests). */
+ * pipelined kernel at any tile count (tests); 4 = as 2 without the weight-stationary kernels. */
 int dbsr_set_conv_algo(int algo);
 /* Which kernel dbsr_conv2d would launch for `d` under the current selection: 5 pointwise projection
  * (16-bit 1x1, cin 32..512 a power of two, cout 32 | 64, no residual: merging.py:34), 4 weight-stationary,

@@ -273,13 +273,13 @@ def test_ws_conv_variants(ops_mod, case):
 
 
 @pytest.mark.parametrize('dt', [torch.float16, torch.bfloat16])
-@pytest.mark.parametrize('epi', [(1, False, 0), (0, True, 1)])
+@pytest.mark.parametrize('epi', [(1, False, 0), (0, True, 1), (0, False, 0)])
 def test_ws_tile_heights_bitwise(ops_mod, dt, epi):
     """The weight-stationary kernel's 16x8 tiles (12 frames of 48x48: a 108-tile grid) and 16x16 tiles (26
     frames: 234 tiles) give bitwise the same outputs on the same frames: the tile shape changes which pixels a
     block owns, never the order a pixel's K is summed in (VERDICT r3 next #2)."""
     act, use_res, post = epi
-    gen = torch.Generator().manual_seed(77 + act)
+    gen = torch.Generator().manual_seed(77 + act + 3 * post)
     x = torch.randn(26, 64, 48, 48, generator=gen)
     w = torch.randn(64, 64, 3, 3, generator=gen) / 24.0
     b = torch.randn(64, generator=gen) * 0.1
@@ -289,7 +289,7 @@ def test_ws_tile_heights_bitwise(ops_mod, dt, epi):
         outs[n] = ops_mod.conv2d(x[:n].to(DEV), w.to(DEV), b.to(DEV), padding=1, act=act,
                                  residual=res[:n].to(DEV) if use_res else None, post_act=post, compute_dtype=dt)
         var[n] = ops_mod.conv2d.last_variant
-    assert var[12] == 4001608 and var[26] == 4001616, var
+    assert var == {12: 4001608, 26: 4001616}, var
     assert torch.equal(outs[12], outs[26][:12])
 
 

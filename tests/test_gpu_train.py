@@ -373,6 +373,28 @@ def test_train_forward_follows_replaced_parameters(synth_sd):
     assert float((p2.detach() - pe).abs().max()) <= 1e-3
 
 
+def test_engine_repacks_in_place_after_trainer_step(synth_sd):
+    """after DBSRTrainer.step the inference engine keeps its plans and graphs and re-packs the
+    updated weights into its own buffers; its forward equals a freshly built engine's, bitwise."""
+    from dbsr_amd.burst import synthetic_bursts
+    burst, gt = synthetic_bursts(1, 3, 24, 32, sr_factor=8, seed=31)
+    b, g = burst.to(DEV), gt.to(DEV)
+    net, tr = _trainer(synth_sd, torch.bfloat16)
+    net.eval()
+    with torch.no_grad():
+        p0, _ = net(b)
+    eng = net._engine
+    tr.step(b, g)
+    tr.step(b, g)
+    with torch.no_grad():
+        p1, _ = net(b)
+        assert net._engine is eng and not eng.weights_stale
+        net._engine = None
+        p2, _ = net(b)
+    assert not torch.equal(p0, p1)
+    assert torch.equal(p1, p2)
+
+
 def test_cfg4_training_steps_bf16(synth_sd):
     """configs[3]'s step shape (SyntheticBurst 14 frames, 128x128 -> 1024x1024, bf16; batch 2 here to
     keep the test short): three Adam steps on one batch run, stay finite and lower the loss."""

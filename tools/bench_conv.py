@@ -1,4 +1,4 @@
-"""Microbenchmark of dbsr_conv2d on the cfg2 hot shapes: tiled vs generic kernel, bf16.
+"""Microbenchmark of dbsr_conv2d on the cfg2 hot shapes: kernel selections (dbsr_set_conv_algo) side by side, fp16.
 Usage: python tools/bench_conv.py"""
 import os
 import sys
@@ -9,6 +9,7 @@ from dbsr_amd.engine import NHWC, PackedConv, Plan, cpad  # noqa: E402
 
 SHAPES = [  # name, frames, H, W, cin, cout, k
     ('enc.res 64->64', 112, 48, 48, 64, 64, 3),
+    ('enc.c1 64->64', 112, 48, 48, 64, 64, 3),
     ('enc.out 64->512', 112, 48, 48, 64, 512, 3),
     ('wp.init 192->128', 112, 48, 48, 192, 128, 3),
     ('wp.res 128->128', 112, 48, 48, 128, 128, 3),
@@ -34,7 +35,7 @@ def main():
     args = ap.parse_args()
     algos = [int(a) for a in args.algos.split(',')]
     dev = torch.device('cuda')
-    dt = torch.bfloat16
+    dt = torch.float16
     s = torch.cuda.current_stream().cuda_stream
     for name, F, H, W, cin, cout, k in SHAPES:
         if args.only and args.only not in name:
@@ -56,7 +57,7 @@ def main():
         for algo in algos:
             L.lib().dbsr_set_conv_algo(algo)
             ms = plan.time_ops(s, reps=args.reps)[0][1]
-            out.append('%s %7.1f us %6.1f TF/s' % (['generic', 'tiled', 'auto', 'pipe', 'no-ws'][algo], ms * 1e3, flop / ms / 1e9))
+            out.append('%s %7.1f us %6.1f TF/s' % (['generic', 'tiled', 'auto', 'pipe', 'no-ws', 'ws8'][algo], ms * 1e3, flop / ms / 1e9))
         L.lib().dbsr_set_conv_algo(2)
         print(f'{name:22s} ' + ' | '.join(out))
 

@@ -107,13 +107,30 @@ def audit(so_path):
                     if q < 0 or not re.search(r'\bm0\b', ins[q].split(',')[0]):
                         m0_ok = False
                         break
+                # a barrier reached (in code order, since the previous barrier) by an LDS-DMA of this wave must be
+                # preceded by a vector-memory wait that covers that DMA (s_waitcnt vmcnt(N) with only non-DMA
+                # operations among the N youngest): a barrier that lets a wave pass with its LDS-DMAs in flight lets
+                # other waves read LDS that has not landed
+                drain_ok, outstanding = True, []
+                for t in ins:
+                    if re.match(r'^(buffer|global|flat)_(load|store|atomic)', t):
+                        outstanding.append(bool(DMA_RE.search(t)))
+                    m = re.search(r's_waitcnt.*vmcnt\((\d+)\)', t)
+                    if m:
+                        n = int(m.group(1))
+                        outstanding = outstanding[len(outstanding) - n:] if n else []
+                    elif t.startswith('s_barrier'):
+                        if any(outstanding):
+                            drain_ok = False
+                        outstanding = []
                 wg = md.get('wg_max', 256)
                 waves_per_simd_min = max(1, (wg // 64 + 3) // 4)
                 owns = regs * waves_per_simd_min >= 512 or regs >= 256
                 fits = md.get('lds', 0) <= 160 * 1024
                 declared = hi_v < regs and (hi_a == 0 or hi_a < md.get('agpr', 0))
-                ok = owns and m0_ok and fits and declared
-                rows.append((k, len(dma), regs, hi_v, hi_a, md.get('lds', 0), wg, owns, m0_ok, declared, fits))
+                ok = owns and m0_ok and fits and declared and drain_ok
+                rows.append((k, len(dma), regs, hi_v, hi_a, md.get('lds', 0), wg, owns, m0_ok, declared, fits,
+                             drain_ok))
                 if not ok:
                     bad.append(k)
     return rows, bad
@@ -123,9 +140,9 @@ def main():
     so = sys.argv[1] if len(sys.argv) > 1 else os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                              'deep-rawburst-sr_amd', 'libdbsr_hip.so')
     rows, bad = audit(so)
-    for k, n, regs, hv, ha, lds, wg, owns, m0, dec, fits in rows:
-        print('%-90s dma %3d regs %3d (max v%d a%d) lds %6d wg %3d owns %d m0 %d declared %d lds-ok %d' % (
-            k[:90], n, regs, hv, ha, lds, wg, owns, m0, dec, fits))
+    for k, n, regs, hv, ha, lds, wg, owns, m0, dec, fits, drain in rows:
+        print('%-90s dma %3d regs %3d (max v%d a%d) lds %6d wg %3d owns %d m0 %d declared %d lds-ok %d drain %d' % (
+            k[:90], n, regs, hv, ha, lds, wg, owns, m0, dec, fits, drain))
     print('%d LDS-DMA kernels, %d violations' % (len(rows), len(bad)))
     sys.exit(1 if bad else 0)
 

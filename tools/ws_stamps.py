@@ -26,8 +26,9 @@ def main():
     ap.add_argument('--only', default='enc.res')
     args = ap.parse_args()
     dev = torch.device('cuda')
-    dt = torch.bfloat16
+    dt = torch.float16
     s = torch.cuda.current_stream().cuda_stream
+    L.lib().dbsr_set_conv_algo(5)                  # the 8-wave kernel (the one with stamps)
     fn = L.lib().dbsr_diag_pipe_stamps
     fn.argtypes = [ctypes.c_void_p, ctypes.c_longlong]
     for name, F, H, W, cin, cout, k in SHAPES:
