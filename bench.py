@@ -157,23 +157,24 @@ def train_main(args, world, rank, dev, dist):
     if dist:
         from dbsr_amd.parallel import max_over_ranks
         el = max_over_ranks(el, device=dev)
-    # per-op device times of the step (HIP events, every op re-launched back to back, outside the timed region)
+    # per-op device times of the step (HIP events, every op re-launched back to back, outside the timed region;
+    # --no-op-timing: profiling runs, the step's own replays only)
     plan = tr.plans[(B, N, S, S)]
-    times = plan.time_ops(torch.cuda.current_stream(dev).cuda_stream, reps=3)
+    times = None if args.no_op_timing else plan.time_ops(torch.cuda.current_stream(dev).cuda_stream, reps=3)
     fam = {}
-    for i, (name, ms) in enumerate(times):
+    for i, (fn, _, name, _) in enumerate(plan.ops):
         if name.startswith('sync.'):
             continue
         kind = plan.kernel.get(i) or name.split('.')[0]
         f = fam.setdefault(kind, [0.0, 0.0, 0])
-        f[0] += ms
+        f[0] += times[i][1] if times is not None else 0.0
         f[1] += plan.work[i][1] if (i in plan.work and plan.work[i][0] == 'flop') else 0.0
         f[2] += 1
     step_flop = sum(w for _, w, _ in fam.values())
     ms_step = el / args.steps * 1e3
     peak_t = PEAK_MFMA_TFLOPS[args.dtype]
     step_tf = step_flop / (ms_step * 1e-3) / 1e12
-    if args.kernel_breakdown and rank == 0:
+    if args.kernel_breakdown and rank == 0 and times is not None:
         for i, (name, ms) in enumerate(times):
             if name.startswith('sync.'):
                 continue
@@ -187,8 +188,8 @@ def train_main(args, world, rank, dev, dist):
         print(f'sum of op times {sum(t for _, t in times) * 1e3:.1f} us vs step {ms_step * 1e3:.1f} us',
               file=sys.stderr)
     conv_fams = {k: v for k, v in fam.items() if v[1] > 0}
-    dom = max(conv_fams, key=lambda k: conv_fams[k][0])
-    d_ms, d_flop, d_n = conv_fams[dom]
+    dom = max(conv_fams, key=lambda k: conv_fams[k][0]) if times is not None else None
+    d_ms, d_flop, d_n = conv_fams[dom] if dom else (0.0, 0.0, 0)
     if rank == 0:
         print(json.dumps({
             'metric': 'training bursts/sec 14x%dx%d RAW->x8 (configs[3] step shape)' % (S, S),
@@ -204,12 +205,12 @@ def train_main(args, world, rank, dev, dist):
             # timed step time, against the dense MFMA peak of the compute dtype
             'step_roofline': {'bound': 'mfma', 'achieved': round(step_tf, 2), 'peak': peak_t, 'unit': 'TFLOP/s',
                               'frac': round(step_tf / peak_t, 4), 'flop_per_step': step_flop},
-            'roofline': {'bound': 'mfma', 'kernel': '%s family, %d launches per step' % (dom, d_n),
-                         'achieved': round(d_flop / (d_ms * 1e-3) / 1e12, 2), 'peak': peak_t, 'unit': 'TFLOP/s',
-                         'frac': round(d_flop / (d_ms * 1e-3) / 1e12 / peak_t, 4), 'traffic': None},
-            'roofline_families': {k: {'ms': round(ms, 3), 'launches': n,
-                                      'frac': round(w / (ms * 1e-3) / 1e12 / peak_t, 4)}
-                                  for k, (ms, w, n) in conv_fams.items()}}))
+            'roofline': ({'bound': 'mfma', 'kernel': '%s family, %d launches per step' % (dom, d_n),
+                          'achieved': round(d_flop / (d_ms * 1e-3) / 1e12, 2), 'peak': peak_t, 'unit': 'TFLOP/s',
+                          'frac': round(d_flop / (d_ms * 1e-3) / 1e12 / peak_t, 4), 'traffic': None} if dom else None),
+            'roofline_families': ({k: {'ms': round(ms, 3), 'launches': n,
+                                       'frac': round(w / (ms * 1e-3) / 1e12 / peak_t, 4)}
+                                   for k, (ms, w, n) in conv_fams.items()} if dom else None)}))
 
 
 def cpu_baseline(N, H, W, seconds):

@@ -1105,8 +1105,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pipe_kernel(ConvK k, int tiles
     for (int ti = 0; ti < my_tiles; ++ti) {
         for (int c = 0; c < nchunks; ++c, ++s) {
             PIPE_STAMP(2 + s * 5);
+            vm_drain();                 // this wave's pieces of stage s landed ...
             PIPE_STAMP(3 + s * 5);
-            dma_barrier();              // stage s landed (vmcnt(0) + barrier); stage s-1 fully consumed
+            __syncthreads();            // ... and everyone's (barrier); stage s-1 fully consumed
             PIPE_STAMP(4 + s * 5);
             const bool fin = c == 0 && ti > 0;
             if (fin) epilogue(prev);

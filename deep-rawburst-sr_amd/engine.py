@@ -410,6 +410,9 @@ class Plan:
                 continue
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             fn(*args, stream)
+            # the reps queue up behind a spin kernel, so they run back to back on the device: a short kernel
+            # (~10 us) is otherwise timed at the host's launch rate (ctypes + HIP launch per call)
+            torch.cuda._sleep(2_000_000)
             e0.record()
             for _ in range(reps):
                 fn(*args, stream)

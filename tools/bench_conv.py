@@ -18,6 +18,7 @@ SHAPES = [  # name, frames, H, W, cin, cout, k
     ('dec.pre 64->64', 8, 48, 48, 64, 64, 3),
     ('dec.init 512->64', 8, 48, 48, 512, 64, 3),
     ('enc.init 4->64', 112, 48, 48, 4, 64, 3),
+    ('ofe.init 2->64', 112, 48, 48, 2, 64, 3),
     ('proj 512->64 1x1', 104, 48, 48, 512, 64, 1),
     ('pwc.dec2.d4 544->32', 104, 16, 16, 544, 32, 3),
     ('pwc.dec2.flow 576->2', 104, 16, 16, 565, 2, 3),

@@ -28,7 +28,7 @@ def main():
     ap.add_argument('--only', default='enc.res')
     args = ap.parse_args()
     dev = torch.device('cuda')
-    dt = torch.bfloat16
+    dt = torch.float16
     s = torch.cuda.current_stream().cuda_stream
     lib = L.lib()
     fn = lib.dbsr_diag_pipe_stamps

@@ -62,9 +62,9 @@ def main():
     stats = list(csv.DictReader(open(os.path.join(src, 'trace', 'run_kernel_stats.csv'))))
     shutil.copy(os.path.join(src, 'trace', 'run_kernel_stats.csv'), os.path.join(outdir, f'{tag}_kernel_stats.csv'))
     lines = [f'# rocprofv3 summary {tag}', '',
-             'Command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline`',
-             '(fp16, batch 8 x 14 frames x 48x48; includes bench.py\'s per-op timing pass, so call counts are not',
-             'one forward). Full CSV: `%s_kernel_stats.csv`.' % tag, '',
+             'Command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline '
+             '--no-op-timing`', '(fp16, batch 8 x 14 frames x 48x48; graph replays only, so every duration is in-step: '
+             '14 forwards per kernel (warmup + timed)). Full CSV: `%s_kernel_stats.csv`.' % tag, '',
              '| kernel | calls | total ms | avg us | % |', '|---|---|---|---|---|']
     for r in stats[:25]:
         lines.append('| `%s` | %s | %.2f | %.1f | %s |' % (r['Name'][:110], r['Calls'], float(r['TotalDurationNs']) / 1e6,
@@ -99,8 +99,8 @@ def main():
     if os.path.exists(tstats):
         shutil.copy(tstats, os.path.join(outdir, f'{tag}_train_kernel_stats.csv'))
         rows = list(csv.DictReader(open(tstats)))
-        lines += ['', '## Training leg: `rocprofv3 --kernel-trace --stats -- python3 bench.py --mode train --steps 3 '
-                  '--warmup 1`', '(bf16, 8 x 14 x 128x128; includes the per-op timing pass). Full CSV: '
+        lines += ['', '## Training leg: `rocprofv3 --kernel-trace --stats -- python3 bench.py --mode train --steps 4 '
+                  '--warmup 2 --no-op-timing`', '(bf16, 8 x 14 x 128x128; 6 trainer steps, no per-op pass). Full CSV: '
                   '`%s_train_kernel_stats.csv`.' % tag, '',
                   '| kernel | calls | total ms | avg us | % |', '|---|---|---|---|---|']
         for r in rows[:25]:

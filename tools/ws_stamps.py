@@ -28,7 +28,7 @@ def main():
     dev = torch.device('cuda')
     dt = torch.float16
     s = torch.cuda.current_stream().cuda_stream
-    L.lib().dbsr_set_conv_algo(5)                  # the 8-wave kernel (the one with stamps)
+    L.lib().dbsr_set_conv_algo(2)                  # default selection: the weight-stationary kernel (the one with stamps)
     fn = L.lib().dbsr_diag_pipe_stamps
     fn.argtypes = [ctypes.c_void_p, ctypes.c_longlong]
     for name, F, H, W, cin, cout, k in SHAPES:
