@@ -907,18 +907,19 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pipe_kernel(ConvK k, int tiles
     // epilogue variants (compile-time where the forward's convs need them): 1 act(ReLU), 2 conv + residual
     // then ReLU (ResBlock conv2), 3 plain, 4 as 2 followed by a 1x1 head (<= 4 outputs) + ReLU whose fp32
     // NCHW result is the only thing stored (the decoder's last ResBlock + RGB predictor, decoders.py:59-61);
-    // 0 reads act / residual / post_act at run time
+    // 0 reads act / residual / post_act at run time; 5 is 0 for the training dgrad's gate at the 32x16 tile,
+    // whose gate is loaded in the epilogue itself (prefetched like the residual, as 0 does, it spills there)
     constexpr bool HEAD = EPI == 4;
     static_assert(!HEAD || WM == 32, "the head reads all 32 channels of a pixel from one cout tile");
-    const bool has_res = EPI == 2 || HEAD || (EPI == 0 && k.r != nullptr);
+    const bool has_res = EPI == 2 || HEAD || ((EPI == 0 || EPI == 5) && k.r != nullptr);
     auto act1 = [&](float v) {
         if constexpr (EPI == 1) return fmaxf(v, 0.f);
-        else if constexpr (EPI == 0) return apply_act(v, k.act);
+        else if constexpr (EPI == 0 || EPI == 5) return apply_act(v, k.act);
         else return v;
     };
     auto act2 = [&](float v) {
         if constexpr (EPI == 2 || EPI == 4) return fmaxf(v, 0.f);
-        else if constexpr (EPI == 0) return apply_act(v, k.post_act);
+        else if constexpr (EPI == 0 || EPI == 5) return apply_act(v, k.post_act);
         else return v;
     };
 
@@ -941,8 +942,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pipe_kernel(ConvK k, int tiles
 
     // tile descriptors hold wave-uniform values only (scalar registers); the lane's own pixel/cout offset
     // within a tile is the same for every tile
-    // EPI 0 only: the training dgrad's ReLU-backward gate (out *= gate > 0), loaded like the residual
-    const bool has_gate = EPI == 0 && k.gt != nullptr;
+    // EPI 0 / 5: the training dgrad's ReLU-backward gate (out *= gate > 0); 0 loads it like the residual
+    const bool has_gate = (EPI == 0 || EPI == 5) && k.gt != nullptr;
     struct Tile { const T* xf; long long y_off, r_off, g_off; int y0, x0, cb; };
     auto decode = [&](int i) {
         int L = i * grid + pb;
@@ -1025,6 +1026,17 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pipe_kernel(ConvK k, int tiles
     // acc[2h+1][j] -- gets bias + act (+ residual + post-act) and is packed to bf16 for a 16-B store
     // during the next stage's taps; the accumulators restart from zero.
     auto epilogue = [&](const Tile& t) {
+        u32x4_t gl[EPI == 5 ? C::NOUT : 1];             // EPI 5: this tile's gate, all pieces in flight at once
+        if constexpr (EPI == 5) {
+            if (has_gate) {
+#pragma unroll
+                for (int q = 0; q < C::NOUT; ++q) {
+                    const int h = q / C::GW, j = q % C::GW;
+                    const bool ok = t.cb + 32 * h + 8 * g < k.cout;
+                    gl[q] = *(const u32x4_t*)((const T*)k.gt + t.g_off + g_lane + grp_off(j) * k.g_ld + (ok ? 32 * h : 0));
+                }
+            }
+        }
 #pragma unroll
         for (int q = 0; q < C::NOUT; ++q) {
             const int h = q / C::GW, j = q % C::GW;
@@ -1045,9 +1057,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pipe_kernel(ConvK k, int tiles
                     v[2 * e + 1] = act2(v[2 * e + 1] + H16<T>::hi(rq[e]));
                 }
             }
-            if constexpr (EPI == 0) {
+            if constexpr (EPI == 0 || EPI == 5) {
                 if (has_gate) {
-                    const u32x4_t gq = gatev[q];
+                    const u32x4_t gq = EPI == 5 ? gl[EPI == 5 ? q : 0] : gatev[EPI == 0 ? q : 0];
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
                         v[2 * e] = H16<T>::lo(gq[e]) > 0.f ? v[2 * e] : 0.f;
@@ -1214,8 +1226,8 @@ int launch_pipe(const ConvK& k, int n_frames, hipStream_t s) {
     int grid = (int)std::min<long long>(nt, cap);
     grid = (grid + 7) / 8 * 8;
     // compile-time epilogues for the forward's three conv flavours, run-time otherwise
-    int epi = 0;                        // (a gated conv, the training dgrad, takes the run-time epilogue 0)
-    if (k.gt) epi = 0;
+    int epi = 0;                        // (a gated conv, the training dgrad, takes the run-time epilogue 0, or 5
+    if (k.gt) epi = (TW == 32 && TH == 16) ? 5 : 0;   // at the 32x16 tile where 0's prefetched gate spills)
     else if (k.head_cout > 0) epi = 4;
     else if (!k.r && k.act == DBSR_ACT_RELU) epi = 1;
     else if (k.r && k.act == DBSR_ACT_NONE && k.post_act == DBSR_ACT_RELU) epi = 2;
@@ -1230,6 +1242,9 @@ int launch_pipe(const ConvK& k, int n_frames, hipStream_t s) {
         case 1: DBSR_PIPE_LAUNCH(1); break;
         case 2: DBSR_PIPE_LAUNCH(2); break;
         case 3: DBSR_PIPE_LAUNCH(3); break;
+        case 5:
+            if constexpr (TW == 32 && TH == 16) DBSR_PIPE_LAUNCH(5);
+            break;
         default: DBSR_PIPE_LAUNCH(0); break;
     }
 #undef DBSR_PIPE_LAUNCH
@@ -1255,8 +1270,8 @@ int pick_pipe(const dbsr_conv_desc* d) {
     // frame per tile; a tile per block is enough to beat the LDS-tiled kernel on their 128 - 576 channels
     else if (d->cout > 32 && d->out_w == 16 && d->out_h == 16) { cfg = 3; tw = 16; th = 16; wm = 64; }
     // frame widths that are multiples of 32 but not 48 (the training step's 128x128 frames): 32x16 tiles
-    // (not gated: the run-time epilogue's gate registers spill at this tile)
-    else if (d->cout > 32 && d->out_w % 32 == 0 && d->out_h % 16 == 0 && !d->gate.ptr) { cfg = 4; tw = 32; th = 16; wm = 64; }
+    // (gated: epilogue 5, the gate loaded in the epilogue)
+    else if (d->cout > 32 && d->out_w % 32 == 0 && d->out_h % 16 == 0) { cfg = 4; tw = 32; th = 16; wm = 64; }
     if (!cfg || d->out_h % th) return 0;
     const long long nt = (long long)d->n_frames * (d->out_w / tw) * (d->out_h / th) * ((d->cout + wm - 1) / wm);
     return (nt >= (cfg == 3 ? 64 : 256) || g_pipe_enabled == 2) ? cfg : 0;
@@ -1449,10 +1464,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ws_kernel(ConvK k, int tiles_x
     auto epilogue = [&](const Tile& t, int rbuf) {
         u32x4_t gatev[EPI == 5 ? C::GW : 1];
         if constexpr (EPI == 5) {
-            // lanes of a partial cout tile past cout read channel cb (never stored)
+            // lanes of a partial cout tile past cout read the cout tile's first channel instead (never stored;
+            // cb itself can be >= cout, which at the last pixel of the last frame lies past the allocation)
 #pragma unroll
             for (int j = 0; j < C::GW; ++j)
-                gatev[j] = *(const u32x4_t*)((const T*)k.gt + t.g_off + px_off(j) * k.g_ld + (cout_ok ? 8 * g : 0));
+                gatev[j] = *(const u32x4_t*)((const T*)k.gt + t.g_off + px_off(j) * k.g_ld + (cout_ok ? 8 * g : -wc * 32));
         }
         const float4 b0 = *(const float4*)(lbias + wc * 32 + 8 * g);
         const float4 b1 = *(const float4*)(lbias + wc * 32 + 8 * g + 4);

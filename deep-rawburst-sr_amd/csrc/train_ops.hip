@@ -40,6 +40,9 @@ int by_dtype(int dtype, F&& f) {
 // operand; cdna_hip_programming.md T10).  fp32 runs v_mfma_f32_16x16x4_f32 on plain reads (one pixel
 // per lane per MFMA).  Each wave's 64x64 accumulator block is written to its own fp32 partial slot
 // [block][wave][co][ci]; wgrad_reduce sums the slots in a fixed order (deterministic).
+// 1x1 stages the X tile itself (no halo).  The conv's bias gradient db[co] = sum over pixels of dY[co] rides
+// along in the ci-block-0 blocks (bpart != NULL): every thread's dY pieces are one fixed 16-B channel group,
+// summed in fp32 as they go to the LDS, then reduced per block into bpart[block][cout] (fixed order).
 // ------------------------------------------------------------------------------------------------
 constexpr int WG_TH = 8, WG_TW = 16, WG_PX = WG_TH * WG_TW;             // output tile
 // blocks over all (co, ci) tiles, each one fp32 partial slot: one per CU for 64-channel blocks (160+ VGPRs x 9
@@ -72,18 +75,20 @@ __device__ __forceinline__ v4s_t tr16(const unsigned char* lds_byte) {
 template <typename T, int K, int CB>
 __global__ __launch_bounds__(K == 3 ? 576 : 256) void conv_wgrad_kernel(
         int n_frames, int h, int w, dbsr_tensor x, int cin, dbsr_tensor dy, int cout, long long n_units,
-        float* __restrict__ partial) {
+        float* __restrict__ partial, float* __restrict__ bpart) {
     constexpr int NW = K == 3 ? 9 : 4;
     constexpr int NB = CB / 16;                        // 16-channel MFMA blocks per edge
     constexpr int ROWB = WgCfg<T, CB>::ROWB;
-    __shared__ __attribute__((aligned(16))) unsigned char lds[(WG_PX + WG_HPX) * ROWB];
+    constexpr int XW = K == 3 ? WG_HW : WG_TW;         // X tile: the 3x3 halo, or the output tile itself
+    constexpr int XPX = K == 3 ? WG_HPX : WG_PX;
+    __shared__ __attribute__((aligned(16))) unsigned char lds[(WG_PX + XPX) * ROWB];
     unsigned char* ldy = lds;                          // [128 px][CB co]
-    unsigned char* lx = lds + WG_PX * ROWB;            // [180 halo px][CB ci]
+    unsigned char* lx = lds + WG_PX * ROWB;            // [XPX px][CB ci]
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int co0 = blockIdx.y * CB, ci0 = blockIdx.z * CB;
     const int tiles_x = (w + WG_TW - 1) / WG_TW, tiles_y = (h + WG_TH - 1) / WG_TH;
     const long long u0 = n_units * blockIdx.x / gridDim.x, u1 = n_units * (blockIdx.x + 1) / gridDim.x;
-    const int ky = K == 3 ? wave / 3 : 1, kx = K == 3 ? wave % 3 : 1;   // 1x1: centre "tap"
+    const int ky = K == 3 ? wave / 3 : 0, kx = K == 3 ? wave % 3 : 0;   // 1x1: the tile itself
     f32x4_t acc[NB][NB];
 #pragma unroll
     for (int i = 0; i < NB; ++i)
@@ -93,8 +98,14 @@ __global__ __launch_bounds__(K == 3 ? 576 : 256) void conv_wgrad_kernel(
     const int ni = min(NB, (cout - co0 + 15) / 16), nj = min(NB, (cin - ci0 + 15) / 16);
     constexpr int EPP = 16 / (int)sizeof(T);           // elements per 16-B piece
     constexpr int PPR = CB / EPP;                      // pieces per CB-channel row
-    constexpr int PIECES = (WG_PX + WG_HPX) * PPR;
+    constexpr int PIECES = (WG_PX + XPX) * PPR;
     constexpr int PT = (PIECES + NW * 64 - 1) / (NW * 64);   // pieces per thread per tile
+    static_assert((NW * 64) % PPR == 0, "a thread's dY pieces must be one channel group");
+    static_assert(NW * 64 * EPP * 4 <= (WG_PX + XPX) * ROWB, "bias reduction must fit the LDS tile");
+    const bool do_bias = bpart != nullptr && blockIdx.z == 0;   // block-uniform
+    float bs[EPP];
+#pragma unroll
+    for (int e = 0; e < EPP; ++e) bs[e] = 0.f;
     // the next tile's dY / X pieces are loaded into registers while this tile's MFMAs run (software pipeline),
     // then written to the LDS after the barrier that ends them
     constexpr int DIST = CB == 32 ? 2 : 1;             // prefetch distance in tiles (register budget)
@@ -116,8 +127,8 @@ __global__ __launch_bounds__(K == 3 ? 576 : 256) void conv_wgrad_kernel(
                 const int yy = y0 + row / WG_TW, xx = x0 + row % WG_TW, c = co0 + pc * EPP;
                 if (yy < h && xx < w && c < cout) v = *(const u32x4_t*)(dyf + ((long long)yy * w + xx) * dy.ld + c);
             } else if (it < PIECES) {
-                const int hr = row - WG_PX;
-                const int yy = y0 - 1 + hr / WG_HW, xx = x0 - 1 + hr % WG_HW, c = ci0 + pc * EPP;
+                const int hr = row - WG_PX, o = K == 3 ? 1 : 0;
+                const int yy = y0 - o + hr / XW, xx = x0 - o + hr % XW, c = ci0 + pc * EPP;
                 if ((unsigned)yy < (unsigned)h && (unsigned)xx < (unsigned)w && c < cin)
                     v = *(const u32x4_t*)(xf + ((long long)yy * w + xx) * x.ld + c);
             }
@@ -131,6 +142,18 @@ __global__ __launch_bounds__(K == 3 ? 576 : 256) void conv_wgrad_kernel(
             if (it >= PIECES) break;
             const int row = it / PPR, pc = it % PPR;
             *(u32x4_t*)(lds + row * ROWB + pc * 16) = src[k];   // ldy rows, then the lx rows right after them
+            if (do_bias && row < WG_PX) {
+                if constexpr (sizeof(T) == 2) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        bs[2 * q] += H16<T>::lo(src[k][q]);
+                        bs[2 * q + 1] += H16<T>::hi(src[k][q]);
+                    }
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) bs[q] += __uint_as_float(src[k][q]);
+                }
+            }
         }
     };
     auto compute = [&]() {
@@ -148,7 +171,7 @@ __global__ __launch_bounds__(K == 3 ? 576 : 256) void conv_wgrad_kernel(
                     const int kk = 8 * g + 4 * half + q;             // pixel of the k-step, 0..31
                     const int ty_ = 2 * s + kk / 16, tx_ = kk % 16;
                     const unsigned char* arow = ldy + (ty_ * WG_TW + tx_) * ROWB;
-                    const unsigned char* brow = lx + ((ty_ + ky) * WG_HW + tx_ + kx) * ROWB;
+                    const unsigned char* brow = lx + ((ty_ + ky) * XW + tx_ + kx) * ROWB;
 #pragma unroll
                     for (int i = 0; i < NB; ++i) {
                         const v4s_t va = tr16(arow + (i * 16 + 4 * p) * 2);
@@ -173,7 +196,7 @@ __global__ __launch_bounds__(K == 3 ? 576 : 256) void conv_wgrad_kernel(
                     const int kk = k4 * 4 + kq;
                     const int ty_ = 2 * s + kk / 16, tx_ = kk % 16;
                     const float* arow = (const float*)(ldy + (ty_ * WG_TW + tx_) * ROWB);
-                    const float* brow = (const float*)(lx + ((ty_ + ky) * WG_HW + tx_ + kx) * ROWB);
+                    const float* brow = (const float*)(lx + ((ty_ + ky) * XW + tx_ + kx) * ROWB);
                     float av[NB], bv[NB];
 #pragma unroll
                     for (int i = 0; i < NB; ++i) {
@@ -201,6 +224,20 @@ __global__ __launch_bounds__(K == 3 ? 576 : 256) void conv_wgrad_kernel(
             if (u + d + DIST < u1) fetch(u + d + DIST, pre[d]);
             compute();
             __syncthreads();
+        }
+    }
+    if (do_bias) {
+        // the loop's last barrier has freed the LDS: thread t's EPP sums of channel group t % PPR, then channel c
+        // adds the threads of its group in thread order
+        float* red = (float*)lds;
+#pragma unroll
+        for (int e = 0; e < EPP; ++e) red[threadIdx.x * EPP + e] = bs[e];
+        __syncthreads();
+        if ((int)threadIdx.x < CB && co0 + (int)threadIdx.x < cout) {
+            const int c = threadIdx.x, g = c / EPP, e = c % EPP;
+            float t = 0.f;
+            for (int th = g; th < NW * 64; th += PPR) t += red[th * EPP + e];
+            bpart[(long long)blockIdx.x * cout + co0 + c] = t;
         }
     }
     // ---- this wave's partial: C[m = co][n = ci], lane holds co 4(lane>>4)+r of block i, ci lane&15 of block j
@@ -353,6 +390,109 @@ __global__ __launch_bounds__(256) void sum_all_kernel(int n, const float* __rest
         __syncthreads();
     }
     if (threadIdx.x == 0) *out = red[0] * scale;
+}
+
+// ------------------------------------------------------------------------------------------------
+// The decoder's RGB predictor (decoders.py:61: 1x1 conv 32 -> HC, ReLU; HC = 3) on its own in the training
+// step, where the last post-ResBlock's output h must be kept for the backward (the inference forward fuses
+// the predictor into that conv instead: dbsr_conv2d_head).  A thread per pixel, grid-stride:
+//   forward:  out[f][c][r] = ReLU(sum_i w[c][i] h[p][i] + b[c])                (fp32 NCHW)
+//   backward: dh[p][i] = [h[p][i] > 0] * sum_c w[c][i] dp[p][c]                (dgrad, gated by h's ReLU)
+//             dw[c][i] = sum_p dp[p][c] h[p][i], db[c] = sum_p dp[p][c]        (one pass over dp and h)
+// The weight/bias sums are fp32 per thread, then a butterfly per wave, the 4 waves in order per block, and
+// the blocks in order (sum_rows_kernel): deterministic.  Memory-bound: h is read once, dh written once.
+// ------------------------------------------------------------------------------------------------
+constexpr int HEAD_CIN = 32;
+inline int head_blocks(long long npix) {
+    return (int)std::min<long long>(1024, std::max<long long>(1, (npix + 255) / 256));
+}
+
+template <typename T, int HC>
+__global__ __launch_bounds__(256) void head_fwd_kernel(int n, int hw, dbsr_tensor h, const float* __restrict__ w,
+                                                       const float* __restrict__ b, float* __restrict__ out) {
+    __shared__ float sw[HC * HEAD_CIN + HC];
+    for (int i = threadIdx.x; i < HC * HEAD_CIN; i += 256) sw[i] = w[i];
+    if ((int)threadIdx.x < HC) sw[HC * HEAD_CIN + threadIdx.x] = b ? b[threadIdx.x] : 0.f;
+    __syncthreads();
+    const long long total = (long long)n * hw;
+    for (long long p = blockIdx.x * 256LL + threadIdx.x; p < total; p += (long long)gridDim.x * 256) {
+        const int f = (int)(p / hw), r = (int)(p - (long long)f * hw);
+        const T* hp = img_ptr<T>(h, f) + (long long)r * h.ld;
+        float v[4][8];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) load8(hp + 8 * g, v[g]);
+        float a[HC];
+#pragma unroll
+        for (int c = 0; c < HC; ++c) a[c] = sw[HC * HEAD_CIN + c];
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+#pragma unroll
+                for (int c = 0; c < HC; ++c) a[c] += sw[c * HEAD_CIN + 8 * g + j] * v[g][j];
+#pragma unroll
+        for (int c = 0; c < HC; ++c) out[((long long)f * HC + c) * hw + r] = fmaxf(a[c], 0.f);
+    }
+}
+
+template <typename T, int HC>
+__global__ __launch_bounds__(256) void head_bwd_kernel(int n, int hw, dbsr_tensor h, dbsr_tensor dp,
+                                                       const float* __restrict__ w, dbsr_tensor dh,
+                                                       float* __restrict__ pw, float* __restrict__ pb) {
+    constexpr int NV = HC * HEAD_CIN + HC;             // dw then db
+    __shared__ float sw[HC * HEAD_CIN];
+    __shared__ float red[4][NV];
+    for (int i = threadIdx.x; i < HC * HEAD_CIN; i += 256) sw[i] = w[i];
+    __syncthreads();
+    float aw[HC][HEAD_CIN], ab[HC];
+#pragma unroll
+    for (int c = 0; c < HC; ++c) {
+        ab[c] = 0.f;
+#pragma unroll
+        for (int i = 0; i < HEAD_CIN; ++i) aw[c][i] = 0.f;
+    }
+    const long long total = (long long)n * hw;
+    for (long long p = blockIdx.x * 256LL + threadIdx.x; p < total; p += (long long)gridDim.x * 256) {
+        const int f = (int)(p / hw), r = (int)(p - (long long)f * hw);
+        const T* hp = img_ptr<T>(h, f) + (long long)r * h.ld;
+        T* op = img_ptr<T>(dh, f) + (long long)r * dh.ld;
+        float d8[8], v[4][8];
+        load8(img_ptr<T>(dp, f) + (long long)r * dp.ld, d8);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) load8(hp + 8 * g, v[g]);
+#pragma unroll
+        for (int c = 0; c < HC; ++c) ab[c] += d8[c];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            float o[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int i = 8 * g + j;
+                float sacc = 0.f;
+#pragma unroll
+                for (int c = 0; c < HC; ++c) {
+                    sacc += sw[c * HEAD_CIN + i] * d8[c];
+                    aw[c][i] += d8[c] * v[g][j];
+                }
+                o[j] = v[g][j] > 0.f ? sacc : 0.f;
+            }
+            store8(op + 8 * g, o);
+        }
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        float x = k < HC * HEAD_CIN ? aw[k / HEAD_CIN][k % HEAD_CIN] : ab[k - HC * HEAD_CIN];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+        if (lane == 0) red[wave][k] = x;
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < NV; k += 256) {
+        const float t = ((red[0][k] + red[1][k]) + red[2][k]) + red[3][k];
+        if (k < HC * HEAD_CIN) pw[(long long)blockIdx.x * HC * HEAD_CIN + k] = t;
+        else pb[(long long)blockIdx.x * HC + (k - HC * HEAD_CIN)] = t;
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -896,18 +1036,30 @@ __global__ void dgrad_weights_kernel(const float* __restrict__ w, int cout, int 
 // ================================================================================================
 static int wgrad_cb(int cin, int cout) { return (cin <= 32 && cout <= 32) ? 32 : 64; }
 
-extern "C" size_t dbsr_conv_wgrad_workspace_bytes(int n_frames, int h, int w, int cin, int cout, int k) {
-    if (n_frames <= 0 || h <= 0 || w <= 0 || cin <= 0 || cout <= 0 || (k != 1 && k != 3)) return 0;
+static long long wgrad_nbx(int n_frames, int h, int w, int cin, int cout) {
     const int cb = wgrad_cb(cin, cout);
     const long long units = (long long)n_frames * ((h + WG_TH - 1) / WG_TH) * ((w + WG_TW - 1) / WG_TW);
     const int nty = (cout + cb - 1) / cb, ntz = (cin + cb - 1) / cb;
-    const long long nbx = std::max<long long>(1, std::min<long long>(units, std::max(1, wg_blocks(cb) / (nty * ntz))));
-    const int nw = k == 3 ? 9 : 4;
-    return (size_t)nbx * nty * ntz * nw * cb * cb * sizeof(float);
+    return std::max<long long>(1, std::min<long long>(units, std::max(1, wg_blocks(cb) / (nty * ntz))));
 }
 
-extern "C" int dbsr_conv_wgrad(int n_frames, int h, int w, dbsr_tensor x, int cin, dbsr_tensor dy, int cout, int k,
-                               float* dw, int accumulate, void* workspace, size_t workspace_bytes, void* stream) {
+// the weight partial slots, then (256-B aligned) the bias partials [nbx][cout]
+static size_t wgrad_slot_bytes(int n_frames, int h, int w, int cin, int cout, int k) {
+    const int cb = wgrad_cb(cin, cout);
+    const int nty = (cout + cb - 1) / cb, ntz = (cin + cb - 1) / cb;
+    const size_t b = (size_t)wgrad_nbx(n_frames, h, w, cin, cout) * nty * ntz * (k == 3 ? 9 : 4) * cb * cb * sizeof(float);
+    return (b + 255) / 256 * 256;
+}
+
+extern "C" size_t dbsr_conv_wgrad_workspace_bytes(int n_frames, int h, int w, int cin, int cout, int k) {
+    if (n_frames <= 0 || h <= 0 || w <= 0 || cin <= 0 || cout <= 0 || (k != 1 && k != 3)) return 0;
+    return wgrad_slot_bytes(n_frames, h, w, cin, cout, k) +
+           (size_t)wgrad_nbx(n_frames, h, w, cin, cout) * cout * sizeof(float);
+}
+
+extern "C" int dbsr_conv_wgrad_bias(int n_frames, int h, int w, dbsr_tensor x, int cin, dbsr_tensor dy, int cout,
+                                    int k, float* dw, float* db, int accumulate, void* workspace,
+                                    size_t workspace_bytes, void* stream) {
     DBSR_CHECK_ARG(map_ok(x) && map_ok(dy) && dw && workspace, "conv_wgrad: null pointer");
     DBSR_CHECK_ARG(x.dtype == dy.dtype, "conv_wgrad: x and dy dtypes differ");
     DBSR_CHECK_ARG(k == 1 || k == 3, "conv_wgrad: k must be 1 or 3 (stride 1, pad k/2)");
@@ -921,9 +1073,10 @@ extern "C" int dbsr_conv_wgrad(int n_frames, int h, int w, dbsr_tensor x, int ci
     const long long units = (long long)n_frames * ((h + WG_TH - 1) / WG_TH) * ((w + WG_TW - 1) / WG_TW);
     const int cb = wgrad_cb(cin, cout);
     const int nty = (cout + cb - 1) / cb, ntz = (cin + cb - 1) / cb;
-    const int nbx = (int)std::max<long long>(1, std::min<long long>(units, std::max(1, wg_blocks(cb) / (nty * ntz))));
+    const int nbx = (int)wgrad_nbx(n_frames, h, w, cin, cout);
     const int nw = k == 3 ? 9 : 4;
     float* part = (float*)workspace;
+    float* bpart = db ? (float*)((char*)workspace + wgrad_slot_bytes(n_frames, h, w, cin, cout, k)) : nullptr;
     hipStream_t s = (hipStream_t)stream;
     // the channel slice is folded into the base pointers
     dbsr_tensor xx = x, dd = dy;
@@ -935,7 +1088,7 @@ extern "C" int dbsr_conv_wgrad(int n_frames, int h, int w, dbsr_tensor x, int ci
     int rc = by_dtype(x.dtype, [&](auto* tag) {
         using T = std::remove_pointer_t<decltype(tag)>;
 #define DBSR_WG(KK, CBB) hipLaunchKernelGGL((conv_wgrad_kernel<T, KK, CBB>), grid, dim3(KK == 3 ? 576 : 256), 0, s, \
-                                           n_frames, h, w, xx, cin, dd, cout, units, part)
+                                           n_frames, h, w, xx, cin, dd, cout, units, part, bpart)
         if (k == 3) {
             if (cb == 32) DBSR_WG(3, 32); else DBSR_WG(3, 64);
         } else {
@@ -949,8 +1102,85 @@ extern "C" int dbsr_conv_wgrad(int n_frames, int h, int w, dbsr_tensor x, int ci
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)(cout * k * k * ((cin + 63) / 64))), dim3(256), 0, s, nbx,
                        nty, ntz, nw, k * k, cout, cin, cb, part, dw, accumulate);
     DBSR_LAUNCH_CHECK();
+    if (db) {
+        hipLaunchKernelGGL(sum_rows_kernel, dim3((unsigned)((cout + 63) / 64)), dim3(256), 0, s, nbx, cout,
+                           (const float*)bpart, db, accumulate, 1.0f);
+        DBSR_LAUNCH_CHECK();
+    }
     return 0;
 }
+
+extern "C" int dbsr_conv_wgrad(int n_frames, int h, int w, dbsr_tensor x, int cin, dbsr_tensor dy, int cout, int k,
+                               float* dw, int accumulate, void* workspace, size_t workspace_bytes, void* stream) {
+    return dbsr_conv_wgrad_bias(n_frames, h, w, x, cin, dy, cout, k, dw, nullptr, accumulate, workspace,
+                                workspace_bytes, stream);
+}
+
+// ================================================================================================
+// predictor head (training step)
+static int head_check(int n, int hw, const dbsr_tensor& h, int cin, int hc) {
+    DBSR_CHECK_ARG(n > 0 && hw > 0 && map_ok(h), "head: bad sizes or null h");
+    DBSR_CHECK_ARG(cin == HEAD_CIN, "head: cin must be %d (the decoder's 32-channel post-ResBlocks)", HEAD_CIN);
+    DBSR_CHECK_ARG(hc >= 1 && hc <= 4, "head: head_cout must be 1..4");
+    const int epp = h.dtype == DBSR_F32 ? 4 : 8;
+    DBSR_CHECK_ARG(vec_ok(h, epp) && h.ld >= h.c0 + HEAD_CIN, "head: h ld/c0 must be multiples of 16 B and cover 32");
+    return 0;
+}
+
+#define DBSR_HEAD_HC(HCV, ...) \
+    switch (HCV) { case 1: { constexpr int HC = 1; __VA_ARGS__; } break; case 2: { constexpr int HC = 2; __VA_ARGS__; } break; \
+                   case 3: { constexpr int HC = 3; __VA_ARGS__; } break; default: { constexpr int HC = 4; __VA_ARGS__; } }
+
+extern "C" int dbsr_head_forward(int n, int hw, dbsr_tensor h, int cin, const float* w, const float* b, int hc,
+                                 float* out, void* stream) {
+    if (int rc = head_check(n, hw, h, cin, hc)) return rc;
+    DBSR_CHECK_ARG(w && out, "head_forward: null pointer");
+    hipStream_t s = (hipStream_t)stream;
+    const int nb = head_blocks((long long)n * hw);
+    return by_dtype(h.dtype, [&](auto* tag) {
+        using T = std::remove_pointer_t<decltype(tag)>;
+        DBSR_HEAD_HC(hc, hipLaunchKernelGGL((head_fwd_kernel<T, HC>), dim3(nb), dim3(256), 0, s, n, hw, h, w, b, out))
+        DBSR_LAUNCH_CHECK();
+        return 0;
+    });
+}
+
+extern "C" size_t dbsr_head_backward_workspace_bytes(int n, int hw, int cin, int hc) {
+    if (n <= 0 || hw <= 0 || hc < 1 || hc > 4) return 0;
+    return (size_t)head_blocks((long long)n * hw) * (size_t)(hc * (cin > 0 ? cin : HEAD_CIN) + hc) * sizeof(float);
+}
+
+extern "C" int dbsr_head_backward(int n, int hw, dbsr_tensor h, int cin, dbsr_tensor dp, const float* w, int hc,
+                                  dbsr_tensor dh, float* dw, float* db, int accumulate, void* workspace,
+                                  size_t workspace_bytes, void* stream) {
+    if (int rc = head_check(n, hw, h, cin, hc)) return rc;
+    DBSR_CHECK_ARG(map_ok(dp) && map_ok(dh) && w && dw && workspace, "head_backward: null pointer");
+    DBSR_CHECK_ARG(dp.dtype == h.dtype && dh.dtype == h.dtype, "head_backward: dtypes differ");
+    const int epp = h.dtype == DBSR_F32 ? 4 : 8;
+    DBSR_CHECK_ARG(vec_ok(dp, epp) && dp.ld >= dp.c0 + 8, "head_backward: dp needs 8 readable channels, 16-B aligned");
+    DBSR_CHECK_ARG(vec_ok(dh, epp) && dh.ld >= dh.c0 + HEAD_CIN, "head_backward: dh ld/c0 must be 16-B multiples, >= 32");
+    DBSR_CHECK_ARG(workspace_bytes >= dbsr_head_backward_workspace_bytes(n, hw, cin, hc), "head_backward: workspace too small");
+    hipStream_t s = (hipStream_t)stream;
+    const int nb = head_blocks((long long)n * hw);
+    float* pw = (float*)workspace;
+    float* pb = pw + (size_t)nb * hc * HEAD_CIN;
+    int rc = by_dtype(h.dtype, [&](auto* tag) {
+        using T = std::remove_pointer_t<decltype(tag)>;
+        DBSR_HEAD_HC(hc, hipLaunchKernelGGL((head_bwd_kernel<T, HC>), dim3(nb), dim3(256), 0, s, n, hw, h, dp, w, dh, pw, pb))
+        DBSR_LAUNCH_CHECK();
+        return 0;
+    });
+    if (rc) return rc;
+    hipLaunchKernelGGL(sum_rows_kernel, dim3((unsigned)((hc * HEAD_CIN + 63) / 64)), dim3(256), 0, s, nb, hc * HEAD_CIN,
+                       (const float*)pw, dw, accumulate, 1.0f);
+    DBSR_LAUNCH_CHECK();
+    if (db) {
+        hipLaunchKernelGGL(sum_rows_kernel, dim3(1), dim3(256), 0, s, nb, hc, (const float*)pb, db, accumulate, 1.0f);
+        DBSR_LAUNCH_CHECK();
+    }
+    return 0;
+}
+#undef DBSR_HEAD_HC
 
 extern "C" size_t dbsr_chan_sum_workspace_bytes(int n, int hw, int c) {
     const long long total = (long long)n * hw;

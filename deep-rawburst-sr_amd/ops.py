@@ -169,9 +169,10 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, act=L.ACT_NONE
 # ---------------------------------------------------------------------------------------------------
 # training-step kernels (backward of the ops above; dbsr_hip.h 'training step')
 # ---------------------------------------------------------------------------------------------------
-def conv2d_wgrad(x, dy, k, compute_dtype=torch.float32):
+def conv2d_wgrad(x, dy, k, compute_dtype=torch.float32, with_bias=False):
     """dL/dW of nn.Conv2d(k x k, stride 1, pad k//2) for input x [N,Cin,H,W] and output gradient dy
-    [N,Cout,H,W] (dbsr_conv_wgrad): fp32 [Cout,Cin,k,k]."""
+    [N,Cout,H,W] (dbsr_conv_wgrad): fp32 [Cout,Cin,k,k].  with_bias: also dL/db = dy.sum((0, 2, 3)) from the
+    same pass (dbsr_conv_wgrad_bias), returned as (dw, db)."""
     _need_cuda(x, dy)
     N, Cin, H, W = x.shape
     Cout = dy.shape[1]
@@ -180,9 +181,16 @@ def conv2d_wgrad(x, dy, k, compute_dtype=torch.float32):
     dw = torch.zeros(Cout, Cin, k, k, dtype=torch.float32, device=x.device)
     need = L.lib().dbsr_conv_wgrad_workspace_bytes(N, H, W, Cin, Cout, k)
     ws = torch.empty(max(need // 4, 1), dtype=torch.float32, device=x.device)
-    L.check(L.lib().dbsr_conv_wgrad(N, H, W, L.tensor_desc(xs, ldx), Cin, L.tensor_desc(ds, ldd), Cout, k,
-                                    dw.data_ptr(), 0, ws.data_ptr(), need, L.stream_ptr(x.device)), 'dbsr_conv_wgrad')
-    return dw
+    if not with_bias:
+        L.check(L.lib().dbsr_conv_wgrad(N, H, W, L.tensor_desc(xs, ldx), Cin, L.tensor_desc(ds, ldd), Cout, k,
+                                        dw.data_ptr(), 0, ws.data_ptr(), need, L.stream_ptr(x.device)),
+                'dbsr_conv_wgrad')
+        return dw
+    db = torch.zeros(Cout, dtype=torch.float32, device=x.device)
+    L.check(L.lib().dbsr_conv_wgrad_bias(N, H, W, L.tensor_desc(xs, ldx), Cin, L.tensor_desc(ds, ldd), Cout, k,
+                                         dw.data_ptr(), db.data_ptr(), 0, ws.data_ptr(), need,
+                                         L.stream_ptr(x.device)), 'dbsr_conv_wgrad_bias')
+    return dw, db
 
 
 def conv2d_dgrad(dy, weight, residual=None, gate=None, compute_dtype=torch.float32):

@@ -207,19 +207,18 @@ class DBSRTrainer:
             return w
 
         def wgrad(name, tc, n, h, w, x, xc0, dy, dyc0, xmap=IDENTITY, dymap=IDENTITY, accumulate=0, cin=None, cout=None):
+            """weight gradient, and the bias gradient (when the conv has one) from the same pass over dy"""
             ci = tc.cin if cin is None else cin
             co = tc.cout if cout is None else cout
             need = lib.dbsr_conv_wgrad_workspace_bytes(n, h, w, ci, co, tc.k)
-            plan.add('wgrad.' + name, lib.dbsr_conv_wgrad, n, h, w, x.d(xc0, xmap), ci, dy.d(dyc0, dymap), co, tc.k,
-                     tc.gw, accumulate, ws('wg', need), need, work=('flop', 2.0 * n * h * w * ci * co * tc.k * tc.k))
-            plan.kernel[len(plan.ops) - 1] = 'conv_wgrad'
-
-        def bgrad(name, tc, n, hwp, dy, dyc0, c=None, accumulate=0):
+            work = ('flop', 2.0 * n * h * w * ci * co * tc.k * tc.k)
             if tc.gb is None:
-                return
-            c = tc.cout if c is None else c
-            need = lib.dbsr_chan_sum_workspace_bytes(n, hwp, c)
-            plan.add('bgrad.' + name, lib.dbsr_chan_sum, n, hwp, c, dy.d(dyc0), tc.gb, accumulate, ws('cs', need), need)
+                plan.add('wgrad.' + name, lib.dbsr_conv_wgrad, n, h, w, x.d(xc0, xmap), ci, dy.d(dyc0, dymap), co,
+                         tc.k, tc.gw, accumulate, ws('wg', need), need, work=work)
+            else:
+                plan.add('wgrad.' + name, lib.dbsr_conv_wgrad_bias, n, h, w, x.d(xc0, xmap), ci, dy.d(dyc0, dymap),
+                         co, tc.k, tc.gw, tc.gb, accumulate, ws('wg', need), need, work=work)
+            plan.kernel[len(plan.ops) - 1] = 'conv_wgrad'
 
         # ================= forward with saved activations =================
         for tc in self.tconvs:
@@ -301,11 +300,13 @@ class DBSRTrainer:
             S1 = S0
         post_s = res_fwd('dec.post', self.dec_post, B, (HS, WS), S1, 0, pc)
         h_last = post_s[-1][3] if post_s else S1
-        pred = torch.zeros(B, 3, HS, WS, dtype=torch.float32, device=dev)
-        pdesc = L.tensor_desc(pred, 1, 0, img_stride=3 * HS * WS, dtype=torch.float32)
-        # the predictor in the compute dtype (its dgrad / wgrad need dY in the same dtype)
-        plan.conv('dec.predictor', self.pred.fwd, B, h_last, 0, (HS, WS), None, 0, L.ACT_RELU,
-                  out_mode=L.OUT_NCHW_F32, y_desc=pdesc)
+        hc = self.pred.cout
+        pred = torch.zeros(B, hc, HS, WS, dtype=torch.float32, device=dev)
+        # the predictor on its own (h_last is kept for the backward): fp32 weights, fp32 NCHW out
+        pmod = self.pred.mod
+        plan.add('dec.predictor', lib.dbsr_head_forward, B, HS * WS, h_last.d(0), pc, pmod.weight.data_ptr(),
+                 pmod.bias.data_ptr() if pmod.bias is not None else None, hc, pred.data_ptr(),
+                 work=('flop', 2.0 * B * HS * WS * pc * hc))
         bufs['pred'] = pred
         bufs['offsets'] = offsets
         bufs['gt'] = torch.zeros(B, 3, HS, WS, dtype=torch.float32, device=dev)
@@ -328,8 +329,12 @@ class DBSRTrainer:
         bufs['gpred'] = torch.zeros(B, 3, HS, WS, dtype=torch.float32, device=dev)
         plan.grad_in_op = (lib.dbsr_relu_grad, (B, 3, HS, WS, pred.data_ptr(), bufs['gpred'].data_ptr(), dP.d(0)),
                            'relu_grad', 0)
-        wgrad('dec.predictor', self.pred, B, HS, WS, h_last, 0, dP, 0)
-        bgrad('dec.predictor', self.pred, B, HS * WS, dP, 0)
+        # predictor backward in one pass over dP and h_last: its dgrad gated by h_last's ReLU, weight and bias grads
+        gh = NHWC(B, HS, WS, r8(pc), dt, dev)
+        need = lib.dbsr_head_backward_workspace_bytes(B, HS * WS, pc, hc)
+        plan.add('bwd.dec.predictor', lib.dbsr_head_backward, B, HS * WS, h_last.d(0), pc, dP.d(0),
+                 pmod.weight.data_ptr(), hc, gh.d(0), self.pred.gw, self.pred.gb, 0, ws('hb', need), need,
+                 work=('flop', 4.0 * B * HS * WS * pc * hc))
 
         def res_bwd(name, blocks, saved, n, hw_, g, gc0, gate_first):
             """ResBlock backward (blocks.py:81-96) from g = dL/dy * [y > 0]; returns the gradient w.r.t. the
@@ -340,20 +345,15 @@ class DBSRTrainer:
                 dt_ = NHWC(n, hw_[0], hw_[1], t.ld, dt, dev)
                 plan.conv(f'bwd.{name}{i}.conv2', c2.bwd, n, g, gc0, hw_, dt_, 0, L.ACT_NONE, gate=t)
                 wgrad(f'{name}{i}.conv2', c2, n, hw_[0], hw_[1], t, 0, g, gc0)
-                bgrad(f'{name}{i}.conv2', c2, n, hw_[0] * hw_[1], g, gc0)
                 dx = NHWC(n, hw_[0], hw_[1], t.ld, dt, dev)
                 gate = x if (i > 0 or gate_first) else None
                 plan.conv(f'bwd.{name}{i}.conv1', c1.bwd, n, dt_, 0, hw_, dx, 0, L.ACT_NONE, res=g, rc0=gc0,
                           gate=gate, gc0=xc0 if gate is not None else 0)
                 wgrad(f'{name}{i}.conv1', c1, n, hw_[0], hw_[1], x, xc0, dt_, 0)
-                bgrad(f'{name}{i}.conv1', c1, n, hw_[0] * hw_[1], dt_, 0)
                 plan.keep.extend([dt_, dx])         # launches hold raw pointers: the plan owns every buffer
                 g, gc0 = dx, 0
             return g, gc0
 
-        # predictor dgrad, gated by the last post-ResBlock output
-        gh = NHWC(B, HS, WS, r8(pc), dt, dev)
-        plan.conv('bwd.dec.predictor', self.pred.bwd, B, dP, 0, (HS, WS), gh, 0, L.ACT_NONE, gate=h_last)
         dS1, _ = res_bwd('dec.post', self.dec_post, post_s, B, (HS, WS), gh, 0, gate_first=False)
         if self.blur is not None:
             dS0 = NHWC(B, HS, WS, pc, dt, dev)
@@ -363,14 +363,12 @@ class DBSRTrainer:
         dU = NHWC(B, H, W, self.dec_up.cout, dt, dev)
         plan.add('bwd.dec.unshuffle', lib.dbsr_unshuffle_gate, B, H, W, S, pc, dS0.d(0), S0.d(0), dU.d(0))
         wgrad('dec.upsample', self.dec_up, B, H, W, g_last, 0, dU, 0)
-        bgrad('dec.upsample', self.dec_up, B, H * W, dU, 0)
         gp = NHWC(B, H, W, gd, dt, dev)
         plan.conv('bwd.dec.upsample', self.dec_up.bwd, B, dU, 0, hw, gp, 0, L.ACT_NONE, gate=g_last)
         gi, _ = res_bwd('dec.pre', self.dec_pre, pre_s, B, hw, gp, 0, gate_first=True)
         if not pre_s:
             pass
         wgrad('dec.init', self.dec_init, B, H, W, FUS, 0, gi, 0)
-        bgrad('dec.init', self.dec_init, B, H * W, gi, 0)
         dFUS = NHWC(B, H, W, C, dt, dev)
         plan.conv('bwd.dec.init', self.dec_init.bwd, B, gi, 0, hw, dFUS, 0, L.ACT_NONE)
         mark_bucket([self.pred, self.dec_up, self.dec_init] + [c for blk in self.dec_pre + self.dec_post for c in blk])
@@ -382,26 +380,22 @@ class DBSRTrainer:
                  dFUS.d(0), dLG.d(0), dF0.d(0), dWfF.d(0))
         # weight predictor
         wgrad('wp.out', self.wp_out, F, H, W, q_last, 0, dLG, 0)
-        bgrad('wp.out', self.wp_out, F, H * W, dLG, 0)
         gq = NHWC(F, H, W, qw, dt, dev)
         plan.conv('bwd.wp.out', self.wp_out.bwd, F, dLG, 0, hw, gq, 0, L.ACT_NONE, gate=q_last)
         gq0, _ = res_bwd('wp.res', self.wp_res, wp_s, F, hw, gq, 0, gate_first=True)
         wgrad('wp.init', self.wp_init, F, H, W, WP, 0, gq0, 0)
-        bgrad('wp.init', self.wp_init, F, H * W, gq0, 0)
         dWP = NHWC(F, H, W, 2 * pd + od, dt, dev)
         plan.conv('bwd.wp.init.bd', self.wp_init_bd, F, gq0, 0, hw, dWP, 0, L.ACT_NONE)
         plan.conv('bwd.wp.init.of', self.wp_init_of, F, gq0, 0, hw, dWP, 2 * pd, L.ACT_NONE, gate=WP, gc0=2 * pd)
         # offset-feature extractor (its input, offsets % 1 from the frozen PWC-Net, takes no gradient)
         go, _ = res_bwd('ofe.res', self.ofe_res, ofe_s, F, hw, dWP, 2 * pd, gate_first=True)
         wgrad('ofe.init', self.ofe_init, F, H, W, om, 0, go, 0)
-        bgrad('ofe.init', self.ofe_init, F, H * W, go, 0)
         # merge prep + projection
         dPJ = NHWC(F, H, W, r8(pd), dt, dev)
         plan.add('bwd.merge_prep', lib.dbsr_merge_prep_backward, B, N, H * W, pd, dWP.d(0), PJ.d(0), dPJ.d(0))
         wgrad('proj.ref', self.proj, B, H, W, E, 0, dPJ, 0, xmap=(1, N, 0, 1), dymap=(1, N, 0, 1))
         if P > 0:
             wgrad('proj.oth', self.proj, P, H, W, Wf, 0, dPJ, 0, dymap=(N - 1, N, 1, 1), accumulate=1)
-        bgrad('proj', self.proj, F, H * W, dPJ, 0)
         mark_bucket([self.wp_out, self.wp_init, self.ofe_init, self.proj] +
                     [c for blk in self.wp_res + self.ofe_res for c in blk])
         dEref = NHWC(B, H, W, C, dt, dev)
@@ -419,12 +413,10 @@ class DBSRTrainer:
                  dE.d(0, (1, N, 0, 1)))
         # encoder
         wgrad('enc.out', self.enc_out, F, H, W, e_last, 0, dE, 0)
-        bgrad('enc.out', self.enc_out, F, H * W, dE, 0)
         ge = NHWC(F, H, W, r8(self.enc_init.cout), dt, dev)
         plan.conv('bwd.enc.out', self.enc_out.bwd, F, dE, 0, hw, ge, 0, L.ACT_NONE, gate=e_last)
         ge0, _ = res_bwd('enc.res', self.enc_res, enc_s, F, hw, ge, 0, gate_first=True)
         wgrad('enc.init', self.enc_init, F, H, W, raw, 0, ge0, 0)
-        bgrad('enc.init', self.enc_init, F, H * W, ge0, 0)
         mark_bucket([self.enc_init, self.enc_out] + [c for blk in self.enc_res for c in blk])
         # ---- scratch: one buffer per kind, as large as its largest request ----
         sizes = {}

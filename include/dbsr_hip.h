@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define DBSR_ABI_VERSION 13
+#define DBSR_ABI_VERSION 14
 
 enum { DBSR_F32 = 0, DBSR_BF16 = 1, DBSR_F16 = 2 };
 enum { DBSR_ACT_NONE = 0, DBSR_ACT_RELU = 1, DBSR_ACT_LRELU = 2 };      /* LeakyReLU slope 0.1 */
@@ -293,6 +293,26 @@ int dbsr_color_apply(int n, int h, int w, int bi, const float* ref, const float*
 size_t dbsr_conv_wgrad_workspace_bytes(int n_frames, int h, int w, int cin, int cout, int k);
 int dbsr_conv_wgrad(int n_frames, int h, int w, dbsr_tensor x, int cin, dbsr_tensor dy, int cout, int k,
                     float* dw, int accumulate, void* workspace, size_t workspace_bytes, void* stream);
+/* dbsr_conv_wgrad plus the conv's bias gradient in the same pass over dy (ABI 14): db[co] (+)= sum_p dy[p][co]
+ * (fp32 [cout], deterministic; db NULL = none).  Replaces the weight and bias halves of nn.Conv2d's backward
+ * (torch.nn.grad.conv2d_weight + grad_output.sum((0, 2, 3)), which the reference's training step gets from
+ * autograd: actors/dbsr_actors.py:27-47).  Same workspace as dbsr_conv_wgrad. */
+int dbsr_conv_wgrad_bias(int n_frames, int h, int w, dbsr_tensor x, int cin, dbsr_tensor dy, int cout, int k,
+                         float* dw, float* db, int accumulate, void* workspace, size_t workspace_bytes, void* stream);
+/* The decoder's RGB predictor as the training step runs it (ABI 14; decoders.py:61, a 1x1 conv 32 -> hc plus
+ * ReLU, kept apart from the last post-ResBlock conv because the backward needs that conv's output h):
+ *   dbsr_head_forward:  out (fp32 NCHW [n][hc][hw]) = ReLU(w . h + b); w fp32 [hc][cin] (torch layout), b
+ *                       fp32 [hc] or NULL.
+ *   dbsr_head_backward: dh = [h > 0] * (w^T . dp) (the predictor's dgrad gated by h's ReLU), dw[c][i] (+)=
+ *                       sum_p dp[p][c] h[p][i], db[c] (+)= sum_p dp[p][c] (db NULL = none); deterministic.
+ * h / dh: NHWC (cin == 32, ld/c0 multiples of 16 B); dp: NHWC with 8 readable channels (hc used), as
+ * dbsr_l1_loss_backward writes it.  hc 1..4.  Replace nn.Conv2d(32, 3, 1)'s forward and autograd backward in
+ * the reference's training step (actors/dbsr_actors.py:27-47). */
+int dbsr_head_forward(int n, int hw, dbsr_tensor h, int cin, const float* w, const float* b, int hc, float* out,
+                      void* stream);
+size_t dbsr_head_backward_workspace_bytes(int n, int hw, int cin, int hc);
+int dbsr_head_backward(int n, int hw, dbsr_tensor h, int cin, dbsr_tensor dp, const float* w, int hc, dbsr_tensor dh,
+                       float* dw, float* db, int accumulate, void* workspace, size_t workspace_bytes, void* stream);
 /* out[c] (+)= sum over the n*hw pixels of t[.][c] (conv bias gradient), fp32; deterministic. */
 size_t dbsr_chan_sum_workspace_bytes(int n, int hw, int c);
 int dbsr_chan_sum(int n, int hw, int c, dbsr_tensor t, float* out, int accumulate, void* workspace,

@@ -44,6 +44,12 @@ def test_conv_wgrad(ops, dtype, case):
     F.conv2d(xr, w, padding=k // 2).backward(dyr)
     out = ops.conv2d_wgrad(x.to(DEV), dy.to(DEV), k, compute_dtype=dtype).cpu()
     assert _rel(out, w.grad) <= 1e-4
+    # the bias gradient from the same pass (dbsr_conv_wgrad_bias): the weight gradient is bitwise the same
+    ow, ob = ops.conv2d_wgrad(x.to(DEV), dy.to(DEV), k, compute_dtype=dtype, with_bias=True)
+    assert torch.equal(ow.cpu(), out)
+    db = dyr.sum((0, 2, 3))
+    # fp32 sums of the same (rounded) values in another order: 1e-5 of the channel's absolute sum
+    assert float((ob.cpu() - db).abs().max()) <= 1e-5 * float(dyr.abs().sum((0, 2, 3)).max())
 
 
 @pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
@@ -69,8 +75,11 @@ def test_conv_dgrad_gate_residual(ops, dtype, case):
 
 # (N, Cout, H, W, Cin, expected kernel): the gated (training dgrad) epilogues of the fast kernels -- weight-
 # stationary EPI 5 on 16x8 tiles (12 frames of 48x48) and 16x16 tiles (40 frames of 32x16, 96 dgrad couts: a
-# partial cout tile), and the pipelined kernel's run-time epilogue (48 frames of 48x48, 128 -> 64 channels)
-GATED = [(12, 64, 48, 48, 64, 4), (40, 64, 32, 16, 96, 4), (48, 128, 48, 48, 64, 2)]
+# partial cout tile), the pipelined kernel's run-time epilogue (48 frames of 48x48, 128 -> 64 channels) and its
+# epilogue 5 at the 32x16 tile (64 frames of 32x32: the training step's 128x128 weight-predictor dgrads; 96 dgrad
+# couts: a partial cout tile)
+GATED = [(12, 64, 48, 48, 64, 4), (40, 64, 32, 16, 96, 4), (48, 128, 48, 48, 64, 2), (64, 128, 32, 32, 128, 2),
+         (64, 128, 32, 32, 96, 2)]
 
 
 @pytest.mark.parametrize('case', GATED)
@@ -134,6 +143,49 @@ def test_chan_sum(ops, dtype, case):
     out = ops.chan_sum(t.to(DEV)).cpu()
     ref = t.double().sum(dim=(0, 2, 3))
     assert float((out.double() - ref).abs().max()) <= 1e-4 * float(t.double().abs().sum(dim=(0, 2, 3)).max())
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('case', [(2, 40, 56, 3), (1, 33, 47, 3), (3, 16, 16, 1), (1, 64, 64, 4)])
+def test_head_forward_backward(dtype, case):
+    """The training step's predictor (dbsr_head_forward / dbsr_head_backward; decoders.py:61, 1x1 conv 32 -> hc +
+    ReLU) against torch on the same rounded operands: pred, the gated dgrad, dW and db."""
+    from dbsr_amd import _lib as L
+    from dbsr_amd.ops import _nhwc
+    N, H, W, hc = case
+    gen = torch.Generator().manual_seed(H * 7 + hc)
+    h = torch.randn(N, 32, H, W, generator=gen).to(dtype).float()        # negative entries: the ReLU gate
+    w = torch.randn(hc, 32, 1, 1, generator=gen) * 0.2
+    b = torch.randn(hc, generator=gen) * 0.1
+    dp = torch.randn(N, hc, H, W, generator=gen).to(dtype).float()
+    lib, s = L.lib(), L.stream_ptr(torch.device(DEV))
+    hs, ldh = _nhwc(h.to(DEV), dtype)
+    wd, bd = w.to(DEV).contiguous(), b.to(DEV).contiguous()
+    out = torch.zeros(N, hc, H, W, device=DEV)
+    L.check(lib.dbsr_head_forward(N, H * W, L.tensor_desc(hs, ldh), 32, wd.data_ptr(), bd.data_ptr(), hc,
+                                  out.data_ptr(), s), 'head_forward')
+    ref = F.relu(F.conv2d(h, w, b))
+    assert float((out.cpu() - ref).abs().max()) <= 1e-4 * float(ref.abs().max())
+    dps = torch.zeros(N, H, W, 8, dtype=dtype, device=DEV)
+    dps[..., :hc] = dp.permute(0, 2, 3, 1).to(DEV).to(dtype)
+    dh = torch.zeros(N, H, W, 32, dtype=dtype, device=DEV)
+    dw = torch.zeros(hc, 32, device=DEV)
+    db = torch.zeros(hc, device=DEV)
+    need = lib.dbsr_head_backward_workspace_bytes(N, H * W, 32, hc)
+    wsb = torch.empty(need // 4 + 1, device=DEV)
+    L.check(lib.dbsr_head_backward(N, H * W, L.tensor_desc(hs, ldh), 32, L.tensor_desc(dps, 8), wd.data_ptr(), hc,
+                                   L.tensor_desc(dh, 32), dw.data_ptr(), db.data_ptr(), 0, wsb.data_ptr(), need, s),
+            'head_backward')
+    hh = h.clone().requires_grad_(True)
+    ww = w.clone().requires_grad_(True)
+    bb = b.clone().requires_grad_(True)
+    F.conv2d(hh, ww, bb).backward(dp)
+    gh = hh.grad * (h > 0)
+    got = dh.float().cpu().permute(0, 3, 1, 2)
+    tol = 1e-4 if dtype == torch.float32 else 1e-2                  # dh is stored in the compute dtype
+    assert float((got - gh).abs().max()) <= tol * float(gh.abs().max())
+    assert _rel(dw.cpu(), ww.grad.reshape(hc, 32)) <= 1e-4
+    assert float((db.cpu() - bb.grad).abs().max()) <= 1e-5 * float(dp.abs().sum((0, 2, 3)).max())
 
 
 @pytest.mark.parametrize('case', [(3, 16, 12, 20, 3.0, torch.float32, False),     # random flow: list flushes
