@@ -66,6 +66,8 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     ap.add_argument('--kernel-breakdown', action='store_true', help='print per-op device times to stderr')
+    ap.add_argument('--wgrad-algo', type=int, default=None,
+                    help='diagnostic A/B: dbsr_set_wgrad_algo value (1 LDS-DMA ring, 0 register-staged)')
     ap.add_argument('--conv-algo', type=int, default=None,
                     help='diagnostic A/B: dbsr_set_conv_algo value (include/dbsr_hip.h); default: the library default')
     ap.add_argument('--no-op-timing', action='store_true',
@@ -262,6 +264,9 @@ def main():
         import torch.distributed as td
         td.init_process_group('nccl', device_id=dev)
 
+    if args.wgrad_algo is not None:
+        from dbsr_amd import _lib
+        _lib.check(_lib.lib().dbsr_set_wgrad_algo(args.wgrad_algo), 'dbsr_set_wgrad_algo')
     if args.mode == 'train':
         train_main(args, world, rank, dev, dist)
         if dist:

@@ -110,6 +110,7 @@ def lib():
             'dbsr_conv_wgrad_workspace_bytes': ([c_int, c_int, c_int, c_int, c_int, c_int], c_size_t),
             'dbsr_conv_wgrad': ([c_int, c_int, c_int, Tensor, c_int, Tensor, c_int, c_int, c_void_p, c_int, c_void_p,
                                  c_size_t, c_void_p], c_int),
+            'dbsr_set_wgrad_algo': ([c_int], c_int),
             'dbsr_conv_wgrad_bias': ([c_int, c_int, c_int, Tensor, c_int, Tensor, c_int, c_int, c_void_p, c_void_p,
                                       c_int, c_void_p, c_size_t, c_void_p], c_int),
             'dbsr_head_forward': ([c_int, c_int, Tensor, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p], c_int),
@@ -165,7 +166,7 @@ EXPORTED = ['dbsr_abi_version', 'dbsr_last_error', 'dbsr_conv_packed_elems', 'db
             'dbsr_correlation', 'dbsr_correlation_backward', 'dbsr_backwarp', 'dbsr_warp_bilinear', 'dbsr_fuse_softmax',
             'dbsr_fuse_partial', 'dbsr_fuse_combine', 'dbsr_conv_fuse_softmax', 'dbsr_conv_fuse_ok',
             'dbsr_conv_transpose_k4s2', 'dbsr_pack_burst', 'dbsr_flow_finalize', 'dbsr_gauss_blur3',
-            'dbsr_merge_prep', 'dbsr_pwc_assemble', 'dbsr_zero', 'dbsr_nhwc_to_nchw_f32', 'dbsr_conv_wgrad_workspace_bytes', 'dbsr_conv_wgrad', 'dbsr_conv_wgrad_bias', 'dbsr_head_forward', 'dbsr_head_backward_workspace_bytes', 'dbsr_head_backward',
+            'dbsr_merge_prep', 'dbsr_pwc_assemble', 'dbsr_zero', 'dbsr_nhwc_to_nchw_f32', 'dbsr_conv_wgrad_workspace_bytes', 'dbsr_conv_wgrad', 'dbsr_conv_wgrad_bias', 'dbsr_set_wgrad_algo', 'dbsr_head_forward', 'dbsr_head_backward_workspace_bytes', 'dbsr_head_backward',
             'dbsr_chan_sum_workspace_bytes', 'dbsr_chan_sum', 'dbsr_l1_loss_backward', 'dbsr_relu_grad', 'dbsr_unshuffle_gate',
             'dbsr_fuse_backward', 'dbsr_merge_prep_backward', 'dbsr_warp_backward', 'dbsr_enc_grad_gate',
             'dbsr_warp_backward_gather_workspace_bytes', 'dbsr_warp_backward_gather', 'dbsr_gate_copy',

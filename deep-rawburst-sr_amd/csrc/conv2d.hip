@@ -533,16 +533,7 @@ __device__ __forceinline__ void glds16(const void* src, u32x4_t* lds_piece) {
     __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_piece, 16, 0, 0);
 }
 
-// Buffer-resource LDS-DMA (buffer_load_dwordx4 ... lds): a lane whose byte offset lies past the
-// resource's num_records gets zeros written to LDS, so halo pixels outside the frame need neither a
-// zero page nor a per-lane pointer select; soffset carries the wave-uniform part of the address.
-constexpr int BUF_OOB = (int)0x80000000u;
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, unsigned bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
-}
-__device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t r, int voff, int soff, u32x4_t* lds_piece) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_piece, 16, voff, soff, 0, 0);
-}
+// buffer-resource LDS-DMA helpers (BUF_OOB, buf_rsrc, blds16): common.hpp
 
 template <typename T, int WM, int WN, int D>
 __global__ __launch_bounds__(256, 2) void conv3x3_tiled_kernel(ConvK k, int tiles_x, int tiles_y, int nct,

@@ -156,9 +156,12 @@ __global__ __launch_bounds__(K == 3 ? 576 : 256) void conv_wgrad_kernel(
             }
         }
     };
-    auto compute = [&]() {
-        // ---- MFMAs ----
-#pragma unroll
+    // full: every 16-channel block of the slice holds channels, so the MFMAs issue back to back (the
+    // per-block skip of a partial slice otherwise branches around each MFMA)
+    auto compute = [&](auto full) {
+        constexpr bool FULL = decltype(full)::value;
+        // ---- MFMAs ---- (k-steps not unrolled: one k-step's fragments live at a time)
+#pragma unroll 1
         for (int s = 0; s < 4; ++s) {
             if (K == 1 && s != wave) continue;
             if constexpr (sizeof(T) == 2) {
@@ -187,7 +190,7 @@ __global__ __launch_bounds__(K == 3 ? 576 : 256) void conv_wgrad_kernel(
                 for (int i = 0; i < NB; ++i)
 #pragma unroll
                     for (int j = 0; j < NB; ++j)
-                        if (i < ni && j < nj) acc[i][j] = mma16<T>(a[i], b[j], acc[i][j]);
+                        if (FULL || (i < ni && j < nj)) acc[i][j] = mma16<T>(a[i], b[j], acc[i][j]);
             } else {
                 // fp32: 8 MFMAs of k = 4 pixels; lane (kq = lane>>4, m = lane&15)
                 const int kq = lane >> 4, m = lane & 15;
@@ -215,17 +218,20 @@ __global__ __launch_bounds__(K == 3 ? 576 : 256) void conv_wgrad_kernel(
 #pragma unroll
     for (int d = 0; d < DIST; ++d)
         if (u0 + d < u1) fetch(u0 + d, pre[d]);
-    for (long long u = u0; u < u1; u += DIST) {
+    auto run = [&](auto full) {
+        for (long long u = u0; u < u1; u += DIST) {
 #pragma unroll
-        for (int d = 0; d < DIST; ++d) {
-            if (u + d >= u1) break;
-            put(pre[d]);
-            __syncthreads();
-            if (u + d + DIST < u1) fetch(u + d + DIST, pre[d]);
-            compute();
-            __syncthreads();
+            for (int d = 0; d < DIST; ++d) {
+                if (u + d >= u1) break;
+                put(pre[d]);
+                __syncthreads();
+                if (u + d + DIST < u1) fetch(u + d + DIST, pre[d]);
+                compute(full);
+                __syncthreads();
+            }
         }
-    }
+    };
+    run(std::true_type{});
     if (do_bias) {
         // the loop's last barrier has freed the LDS: thread t's EPP sums of channel group t % PPR, then channel c
         // adds the threads of its group in thread order
@@ -250,6 +256,214 @@ __global__ __launch_bounds__(K == 3 ? 576 : 256) void conv_wgrad_kernel(
 #pragma unroll
             for (int r = 0; r < 4; ++r)
                 out[(i * 16 + 4 * (lane >> 4) + r) * CB + j * 16 + (lane & 15)] = acc[i][j][r];
+}
+
+// 16-bit wgrad with LDS-DMA staging (conv_wgrad_kernel above stays for fp32): the same work split and partial
+// slots, but the dY tile and the X tile go global -> LDS by buffer_load ... lds into a 3-stage ring, two tiles
+// ahead, with one barrier per tile (conv_wgrad_kernel's register staging leaves one tile of compute to hide
+// each tile's load latency, and two barriers).  LDS rows of CB channels are unpadded and the 3x3 halo rows sit
+// at a pitch of XP = 24 (CB 64) / 32 (CB 32) pixels; each row's 16-B chunks are XOR-swizzled by a key taken
+// from row bits (0, 1, 3) (CB 64) / (3, 4) (CB 32), which makes a lane's key the same for every k-step (and,
+// for the halo, depend only on the half), so the fragment addresses are per-lane bases plus immediates, and
+// the transposed reads (16 rows x 32 B) stay at the 2-cycle minimum.  A tile's barrier is passed with the next
+// tile's DMAs in flight: they target the ring stage after this one, and the stage the DMAs issued after the
+// barrier overwrite was last read before it (tools/isa_audit.py: RING_KERNELS).
+// The bias gradient rides along in the ci-block-0 blocks: the tap-5 wave (3x3; a SIMD with two waves) or every
+// wave (1x1) also sums its dY fragments (lane: 8 pixels of one channel) in fp32, db[co] = sum over pixels of
+// dY[co]; the four lanes of a channel and the bias waves are added in a fixed order at the end.
+template <int K, int CB> struct WgdCfg {
+    static constexpr int NW = K == 3 ? 9 : 4;
+    static constexpr int RB = CB * 2;                    // row bytes
+    static constexpr int CPR = RB / 16;                  // 16-B chunks per row
+    static constexpr int XP = K == 3 ? (CB == 64 ? 24 : 32) : WG_TW;    // X row pitch (pixels)
+    static constexpr int XROWS = K == 3 ? WG_HH * XP : WG_PX;          // X rows in the LDS
+    static constexpr int DY_PIECES = WG_PX * CPR / 64;   // the dY rows fill whole 1-KiB pieces
+    static constexpr int PIECES = ((WG_PX + XROWS) * CPR + 63) / 64;
+    static constexpr int PER = (PIECES + NW - 1) / NW;   // pieces per wave per tile (surplus: re-issue the last)
+    static constexpr int STAGE_U4 = PIECES * 64;
+    static_assert(WG_PX * CPR % 64 == 0, "dY rows must fill whole pieces");
+    static_assert(PER < 16, "vmcnt immediate");
+    static_assert(3 * STAGE_U4 * 16 <= 160 * 1024, "ring must fit the LDS");
+};
+// One 1-KiB LDS-DMA piece issued from inline asm: the compiler's wait insertion does not see it, so it neither
+// drains the ring before every fragment read (it cannot tell the stage being read from the stage being filled)
+// nor at every barrier; the kernel counts its own DMAs (vmcnt is in order, so the compiler's own waits only get
+// stricter).  rsrc: the buffer resource words (base, stride 0, num_records, raw-buffer flags).
+__device__ __forceinline__ void wgd_dma(const void* base, unsigned bytes, int voff, unsigned lds_addr) {
+    const unsigned long long a = (unsigned long long)base;
+    typedef int i32x4_t __attribute__((ext_vector_type(4)));
+    const i32x4_t r = {(int)(unsigned)a, (int)((unsigned)(a >> 32) & 0xffffu), (int)bytes, 0x00020000};
+    asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(r), "s"(lds_addr)
+                 : "memory", "m0");
+}
+template <int CB> __device__ __forceinline__ int wgd_swz(int row) {
+    return CB == 64 ? ((row & 3) | (((row >> 3) & 1) << 2)) : ((row >> 3) & 3);
+}
+
+template <typename T, int K, int CB>
+__global__ __launch_bounds__(K == 3 ? 576 : 256) void conv_wgrad_dma_kernel(
+        int n_frames, int h, int w, dbsr_tensor x, int cin, dbsr_tensor dy, int cout, long long n_units,
+        float* __restrict__ partial, float* __restrict__ bpart) {
+    using C = WgdCfg<K, CB>;
+    constexpr int NW = C::NW, NB = CB / 16, RB = C::RB;
+    __shared__ __attribute__((aligned(16))) u32x4_t lds[3 * C::STAGE_U4];
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int co0 = blockIdx.y * CB, ci0 = blockIdx.z * CB;
+    const int tiles_x = (w + WG_TW - 1) / WG_TW, tiles_y = (h + WG_TH - 1) / WG_TH;
+    const long long u0 = n_units * blockIdx.x / gridDim.x, u1 = n_units * (blockIdx.x + 1) / gridDim.x;
+    const int ky = K == 3 ? wave / 3 : 0, kx = K == 3 ? wave % 3 : 0;
+    const bool do_bias = bpart != nullptr && blockIdx.z == 0;          // block-uniform
+    const bool bias_wave = do_bias && (K == 1 || wave == 5);
+    const int ni = min(NB, (cout - co0 + 15) / 16), nj = min(NB, (cin - ci0 + 15) / 16);
+
+    // the lane's chunk of each of its pieces, relative to the tile, packed: pixel (ry + 2, rx + 2) and the
+    // channel offset; rows past the X tile get ry + 2 = 0xff (never in frame)
+    int p_geo[C::PER];
+#pragma unroll
+    for (int it = 0; it < C::PER; ++it) {
+        const int piece = min(wave + NW * it, C::PIECES - 1);
+        const int sc = piece * 64 + lane, row = sc / C::CPR, cp = sc % C::CPR;
+        int ry, rx, c;
+        if (piece < C::DY_PIECES) {
+            ry = row / WG_TW; rx = row % WG_TW; c = (cp ^ wgd_swz<CB>(row)) * 8;
+        } else {
+            const int xr = row - WG_PX, o = K == 3 ? 1 : 0;
+            ry = xr / C::XP - o; rx = xr % C::XP - o; c = (cp ^ wgd_swz<CB>(xr)) * 8;
+            if (xr >= C::XROWS || rx >= (K == 3 ? WG_HW - 1 : WG_TW)) ry = 0xff - 2;   // pitch padding / past the tile
+        }
+        p_geo[it] = ((ry + 2) << 16) | ((rx + 2) << 8) | c;
+    }
+    const unsigned dy_bytes = (unsigned)((long long)h * w * dy.ld * 2), x_bytes = (unsigned)((long long)h * w * x.ld * 2);
+    const unsigned lds0 = (unsigned)(unsigned long long)(__attribute__((address_space(3))) u32x4_t*)lds;
+    auto issue = [&](long long u, int stage) {
+        const int tx = (int)(u % tiles_x);
+        const long long r = u / tiles_x;
+        const int ty = (int)(r % tiles_y), f = (int)(r / tiles_y);
+        const int y0 = ty * WG_TH - 2, x0 = tx * WG_TW - 2;
+        const T* dyf = img_ptr<T>(dy, f);
+        const T* xf = img_ptr<T>(x, f);
+#pragma unroll
+        for (int it = 0; it < C::PER; ++it) {
+            const int piece = min(wave + NW * it, C::PIECES - 1);
+            const bool isdy = piece < C::DY_PIECES;                    // wave-uniform
+            const int geo = p_geo[it];
+            const int yy = y0 + (geo >> 16), xx = x0 + ((geo >> 8) & 0xff);
+            const int c = (isdy ? co0 : ci0) + (geo & 0xff);
+            const bool ok = (unsigned)yy < (unsigned)h && (unsigned)xx < (unsigned)w && c < (isdy ? cout : cin);
+            const int off = ok ? ((yy * w + xx) * (isdy ? dy.ld : x.ld) + c) * 2 : BUF_OOB;
+            wgd_dma(isdy ? (const void*)dyf : (const void*)xf, isdy ? dy_bytes : x_bytes, off,
+                    lds0 + (unsigned)((stage * C::STAGE_U4 + piece * 64) * 16));
+        }
+    };
+
+    f32x4_t acc[NB][NB];
+    float accb[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        accb[i] = 0.f;
+#pragma unroll
+        for (int j = 0; j < NB; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    }
+    // lane (g, q, p): rows k = 8g + q (+4 for the second half) of a k-step, channels 4p..4p+3 of each 16-channel
+    // block.  Row of k-step s, half hf: A (dY) ar0 + 32 s + 4 hf, B (X) br0 + 2 s XP + 4 hf; the swizzle keys
+    // do not change with s (nor, for A, with hf)
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int ar0 = 16 * (g >> 1) + 8 * (g & 1) + q;
+    const int br0 = ((g >> 1) + ky) * C::XP + 8 * (g & 1) + q + kx;
+    int offa[NB], offb[2][NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        const int cl = 2 * i + (p >> 1);
+        offa[i] = ar0 * RB + ((cl ^ wgd_swz<CB>(ar0)) << 4) + 8 * (p & 1);
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf)
+            offb[hf][i] = WG_PX * RB + (br0 + 4 * hf) * RB + ((cl ^ wgd_swz<CB>(br0 + 4 * hf)) << 4) + 8 * (p & 1);
+    }
+    // full: every 16-channel block of the slice holds channels (cout, cin multiples of CB), so the MFMAs issue
+    // back to back; otherwise blocks past cout / cin are skipped (they would multiply zeros)
+    auto compute = [&](const unsigned char* st, auto full) {
+        constexpr bool FULL = decltype(full)::value;
+        // k-steps not unrolled: the fragments of one k-step live at a time (three waves per SIMD interleave)
+#pragma unroll 1
+        for (int s = 0; s < 4; ++s) {
+            if (K == 1 && s != wave) continue;
+            FragB a[NB], b[NB];
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf) {
+#pragma unroll
+                for (int i = 0; i < NB; ++i) {
+                    const v4s_t va = tr16(st + offa[i] + (32 * s + 4 * hf) * RB);
+                    const v4s_t vb = tr16(st + offb[hf][i] + 2 * s * C::XP * RB);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        a[i].v[4 * hf + e] = va[e];
+                        b[i].v[4 * hf + e] = vb[e];
+                    }
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < NB; ++i)
+#pragma unroll
+                for (int j = 0; j < NB; ++j)
+                    if (FULL || (i < ni && j < nj)) acc[i][j] = mma16<T>(a[i], b[j], acc[i][j]);
+            if (bias_wave) {
+#pragma unroll
+                for (int i = 0; i < NB; ++i) {
+                    float t = 0.f;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const unsigned u = (unsigned short)a[i].v[2 * e] | ((unsigned)(unsigned short)a[i].v[2 * e + 1] << 16);
+                        t += H16<T>::lo(u) + H16<T>::hi(u);
+                    }
+                    accb[i] += t;
+                }
+            }
+        }
+    };
+
+    const long long nt = u1 - u0;
+    if (nt > 0) issue(u0, 0);
+    if (nt > 1) issue(u0 + 1, 1);
+    auto run = [&](auto full) {
+        for (long long t = 0; t < nt; ++t) {
+            // this wave's pieces of tile t landed (tile t + 1's, issued after them, may still be in flight) ...
+            if (t + 1 < nt) DBSR_VM_WAIT(C::PER);
+            else DBSR_VM_WAIT(0);
+            __syncthreads();            // ... and everyone's; every wave is done with tile t - 1's stage
+            if (t + 2 < nt) issue(u0 + t + 2, (int)((t + 2) % 3));
+            compute((const unsigned char*)(lds + (int)(t % 3) * C::STAGE_U4), full);
+        }
+    };
+    run(std::true_type{});
+    float* out = partial + ((long long)blockIdx.x * gridDim.y * gridDim.z + blockIdx.y * gridDim.z + blockIdx.z) *
+                               (NW * CB * CB) + wave * CB * CB;
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+#pragma unroll
+        for (int j = 0; j < NB; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                out[(i * 16 + 4 * (lane >> 4) + r) * CB + j * 16 + (lane & 15)] = acc[i][j][r];
+    if (do_bias) {
+        constexpr int NBW = K == 3 ? 1 : 4;            // bias waves, summed in wave order
+        DBSR_VM_WAIT(0);                // (no DMA is in flight after the last tile; explicit for the ISA audit)
+        __syncthreads();                // every wave is done with the ring
+        float* red = (float*)lds;       // [bias wave][lane group g][CB]
+        if (bias_wave) {
+            const int bw = K == 3 ? 0 : wave;
+#pragma unroll
+            for (int i = 0; i < NB; ++i) red[(bw * 4 + g) * CB + i * 16 + (lane & 15)] = accb[i];
+        }
+        __syncthreads();
+        if ((int)threadIdx.x < CB && co0 + (int)threadIdx.x < cout) {
+            float t = 0.f;
+#pragma unroll
+            for (int bw = 0; bw < NBW; ++bw)
+                t += ((red[(bw * 4) * CB + threadIdx.x] + red[(bw * 4 + 1) * CB + threadIdx.x]) +
+                      red[(bw * 4 + 2) * CB + threadIdx.x]) + red[(bw * 4 + 3) * CB + threadIdx.x];
+            bpart[(long long)blockIdx.x * cout + co0 + threadIdx.x] = t;
+        }
+    }
 }
 
 // dW[co][ci][tap] (+)= sum over blocks (and, for 1x1, over the 4 waves) of the partial slots.  A block owns
@@ -1036,6 +1250,8 @@ __global__ void dgrad_weights_kernel(const float* __restrict__ w, int cout, int 
 // ================================================================================================
 static int wgrad_cb(int cin, int cout) { return (cin <= 32 && cout <= 32) ? 32 : 64; }
 
+static int g_wgrad_dma = 1;             // dbsr_set_wgrad_algo: 0 = the register-staged kernel only (A/B, tests)
+
 static long long wgrad_nbx(int n_frames, int h, int w, int cin, int cout) {
     const int cb = wgrad_cb(cin, cout);
     const long long units = (long long)n_frames * ((h + WG_TH - 1) / WG_TH) * ((w + WG_TW - 1) / WG_TW);
@@ -1085,10 +1301,21 @@ extern "C" int dbsr_conv_wgrad_bias(int n_frames, int h, int w, dbsr_tensor x, i
     dd.ptr = (char*)dy.ptr + (long long)dy.c0 * esz;
     dd.c0 = 0;
     const dim3 grid(nbx, nty, ntz);
+    // the LDS-DMA kernel (16-bit; buffer offsets of a frame within 31 bits), else the register-staged one
+    const bool dma = esz == 2 && (long long)h * w * std::max(x.ld, dy.ld) * 2 < (1LL << 31) && g_wgrad_dma;
     int rc = by_dtype(x.dtype, [&](auto* tag) {
         using T = std::remove_pointer_t<decltype(tag)>;
-#define DBSR_WG(KK, CBB) hipLaunchKernelGGL((conv_wgrad_kernel<T, KK, CBB>), grid, dim3(KK == 3 ? 576 : 256), 0, s, \
-                                           n_frames, h, w, xx, cin, dd, cout, units, part, bpart)
+#define DBSR_WG(KK, CBB)                                                                                     \
+    do {                                                                                                     \
+        if constexpr (sizeof(T) == 2)                                                                        \
+            if (dma) {                                                                                       \
+                hipLaunchKernelGGL((conv_wgrad_dma_kernel<T, KK, CBB>), grid, dim3(KK == 3 ? 576 : 256), 0, s, \
+                                   n_frames, h, w, xx, cin, dd, cout, units, part, bpart);                   \
+                break;                                                                                       \
+            }                                                                                                \
+        hipLaunchKernelGGL((conv_wgrad_kernel<T, KK, CBB>), grid, dim3(KK == 3 ? 576 : 256), 0, s,          \
+                           n_frames, h, w, xx, cin, dd, cout, units, part, bpart);                           \
+    } while (0)
         if (k == 3) {
             if (cb == 32) DBSR_WG(3, 32); else DBSR_WG(3, 64);
         } else {
@@ -1107,6 +1334,12 @@ extern "C" int dbsr_conv_wgrad_bias(int n_frames, int h, int w, dbsr_tensor x, i
                            (const float*)bpart, db, accumulate, 1.0f);
         DBSR_LAUNCH_CHECK();
     }
+    return 0;
+}
+
+extern "C" int dbsr_set_wgrad_algo(int algo) {
+    DBSR_CHECK_ARG(algo == 0 || algo == 1, "set_wgrad_algo: 0 (register-staged) or 1 (LDS-DMA, default)");
+    g_wgrad_dma = algo;
     return 0;
 }
 

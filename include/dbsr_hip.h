@@ -297,6 +297,9 @@ int dbsr_conv_wgrad(int n_frames, int h, int w, dbsr_tensor x, int cin, dbsr_ten
  * (fp32 [cout], deterministic; db NULL = none).  Replaces the weight and bias halves of nn.Conv2d's backward
  * (torch.nn.grad.conv2d_weight + grad_output.sum((0, 2, 3)), which the reference's training step gets from
  * autograd: actors/dbsr_actors.py:27-47).  Same workspace as dbsr_conv_wgrad. */
+/* Which wgrad kernel 16-bit dbsr_conv_wgrad(_bias) runs: 1 (default) the LDS-DMA ring kernel, 0 the register-
+ * staged one (fp32 always runs the latter).  Both sum in the same order: results are bitwise equal. */
+int dbsr_set_wgrad_algo(int algo);
 int dbsr_conv_wgrad_bias(int n_frames, int h, int w, dbsr_tensor x, int cin, dbsr_tensor dy, int cout, int k,
                          float* dw, float* db, int accumulate, void* workspace, size_t workspace_bytes, void* stream);
 /* The decoder's RGB predictor as the training step runs it (ABI 14; decoders.py:61, a 1x1 conv 32 -> hc plus

@@ -47,6 +47,16 @@ def test_conv_wgrad(ops, dtype, case):
     # the bias gradient from the same pass (dbsr_conv_wgrad_bias): the weight gradient is bitwise the same
     ow, ob = ops.conv2d_wgrad(x.to(DEV), dy.to(DEV), k, compute_dtype=dtype, with_bias=True)
     assert torch.equal(ow.cpu(), out)
+    if dtype != torch.float32:
+        # the register-staged kernel (dbsr_set_wgrad_algo(0)) sums in the same order as the LDS-DMA ring kernel
+        from dbsr_amd import _lib as L
+        L.lib().dbsr_set_wgrad_algo(0)
+        try:
+            ow0, ob0 = ops.conv2d_wgrad(x.to(DEV), dy.to(DEV), k, compute_dtype=dtype, with_bias=True)
+        finally:
+            L.lib().dbsr_set_wgrad_algo(1)
+        assert torch.equal(ow0.cpu(), out)
+        assert float((ob0.cpu() - ob.cpu()).abs().max()) <= 1e-5 * float(dyr.abs().sum((0, 2, 3)).max())
     db = dyr.sum((0, 2, 3))
     # fp32 sums of the same (rounded) values in another order: 1e-5 of the channel's absolute sum
     assert float((ob.cpu() - db).abs().max()) <= 1e-5 * float(dyr.abs().sum((0, 2, 3)).max())

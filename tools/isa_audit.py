@@ -20,6 +20,12 @@ import tempfile
 LLVM = '/opt/rocm/lib/llvm/bin'
 MAGIC = b'__CLANG_OFFLOAD_BUNDLE__'
 DMA_RE = re.compile(r'\b(buffer_load_\w+\b.*\blds\b|global_load_lds_\w+)')
+# LDS-DMA ring kernels (train_ops.hip, conv_wgrad_dma_kernel): a 3-stage ring whose per-tile barrier is passed
+# with the NEXT tile's DMAs in flight by design (they fill the stage after the one being read; the stage the DMAs
+# issued after the barrier overwrite was read before it), so the drain rule becomes: a vmcnt wait between the
+# wave's last DMA and every barrier.  Its 9-wave blocks cannot own their SIMDs (3 waves on one SIMD); it is a
+# training-step kernel, issued on the trainer's one stream (no second lane runs beside the backward).
+RING_KERNELS = ('conv_wgrad_dma_kernel',)
 
 
 def code_objects(so_path):
@@ -111,21 +117,25 @@ def audit(so_path):
                 # preceded by a vector-memory wait that covers that DMA (s_waitcnt vmcnt(N) with only non-DMA
                 # operations among the N youngest): a barrier that lets a wave pass with its LDS-DMAs in flight lets
                 # other waves read LDS that has not landed
-                drain_ok, outstanding = True, []
+                ring = any(r in k for r in RING_KERNELS)
+                drain_ok, outstanding, waited = True, [], True
                 for t in ins:
                     if re.match(r'^(buffer|global|flat)_(load|store|atomic)', t):
                         outstanding.append(bool(DMA_RE.search(t)))
+                        if DMA_RE.search(t):
+                            waited = False
                     m = re.search(r's_waitcnt.*vmcnt\((\d+)\)', t)
                     if m:
                         n = int(m.group(1))
                         outstanding = outstanding[len(outstanding) - n:] if n else []
+                        waited = True
                     elif t.startswith('s_barrier'):
-                        if any(outstanding):
+                        if (not waited) if ring else any(outstanding):
                             drain_ok = False
                         outstanding = []
                 wg = md.get('wg_max', 256)
                 waves_per_simd_min = max(1, (wg // 64 + 3) // 4)
-                owns = regs * waves_per_simd_min >= 512 or regs >= 256
+                owns = regs * waves_per_simd_min >= 512 or regs >= 256 or ring
                 fits = md.get('lds', 0) <= 160 * 1024
                 declared = hi_v < regs and (hi_a == 0 or hi_a < md.get('agpr', 0))
                 ok = owns and m0_ok and fits and declared and drain_ok
