@@ -875,21 +875,55 @@ __global__ __launch_bounds__(256) void fuse_bwd_kernel(int B, int N, int hw, int
     float fu[8], dfu[8];
     load8(img_ptr<T>(fused, b) + (long long)rr * fused.ld + c, fu);
     load8(img_ptr<T>(dfused, b) + (long long)rr * dfused.ld + c, dfu);
-    for (int n = 0; n < N; ++n) {
-        float wv[8], fv[8], dl[8], df[8];
-        load8(img_ptr<T>(wts, b * N + n) + (long long)rr * wts.ld + c, wv);
-        const T* fp = n == 0 ? img_ptr<T>(ref, b) + (long long)rr * ref.ld
-                             : img_ptr<T>(oth, b * (N - 1) + n - 1) + (long long)rr * oth.ld;
-        load8(fp + c, fv);
+    // frames in chunks of FB: every load of a chunk is issued before its first store (the stores may alias the
+    // inputs as far as the compiler knows, so a load after a store waits for it: one latency per frame before)
+    constexpr int FB = 7;
+    constexpr int RW = sizeof(T) == 2 ? 1 : 2;           // 16-B words per 8 elements
+    for (int n0 = 0; n0 < N; n0 += FB) {
+        u32x4_t wr[FB][RW], fr[FB][RW];                  // raw: converted when used (half the registers)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            df[j] = wv[j] * dfu[j];
-            dl[j] = df[j] * (fv[j] - fu[j]);
+        for (int u = 0; u < FB; ++u) {
+            const int n = n0 + u;
+            if (n < N) {
+                const T* wp = img_ptr<T>(wts, b * N + n) + (long long)rr * wts.ld + c;
+                const T* fp = (n == 0 ? img_ptr<T>(ref, b) + (long long)rr * ref.ld
+                                      : img_ptr<T>(oth, b * (N - 1) + n - 1) + (long long)rr * oth.ld) + c;
+#pragma unroll
+                for (int q4 = 0; q4 < RW; ++q4) {
+                    wr[u][q4] = *(const u32x4_t*)(wp + q4 * (8 / RW));
+                    fr[u][q4] = *(const u32x4_t*)(fp + q4 * (8 / RW));
+                }
+            }
         }
-        store8(img_ptr<T>(dlogits, b * N + n) + (long long)rr * dlogits.ld + c, dl);
-        T* dp = n == 0 ? img_ptr<T>(dref, b) + (long long)rr * dref.ld
-                       : img_ptr<T>(doth, b * (N - 1) + n - 1) + (long long)rr * doth.ld;
-        store8(dp + c, df);
+#pragma unroll
+        for (int u = 0; u < FB; ++u) {
+            const int n = n0 + u;
+            if (n >= N) break;
+            float wv[8], fv[8];
+            if constexpr (sizeof(T) == 2) {
+#pragma unroll
+                for (int q4 = 0; q4 < 4; ++q4) {
+                    wv[2 * q4] = H16<T>::lo(wr[u][0][q4]); wv[2 * q4 + 1] = H16<T>::hi(wr[u][0][q4]);
+                    fv[2 * q4] = H16<T>::lo(fr[u][0][q4]); fv[2 * q4 + 1] = H16<T>::hi(fr[u][0][q4]);
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    wv[j] = __uint_as_float(wr[u][j / 4][j % 4]);
+                    fv[j] = __uint_as_float(fr[u][j / 4][j % 4]);
+                }
+            }
+            float dl[8], df[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                df[j] = wv[j] * dfu[j];
+                dl[j] = df[j] * (fv[j] - fu[j]);
+            }
+            store8(img_ptr<T>(dlogits, b * N + n) + (long long)rr * dlogits.ld + c, dl);
+            T* dp = n == 0 ? img_ptr<T>(dref, b) + (long long)rr * dref.ld
+                           : img_ptr<T>(doth, b * (N - 1) + n - 1) + (long long)rr * doth.ld;
+            store8(dp + c, df);
+        }
     }
 }
 
