@@ -336,9 +336,11 @@ __global__ __launch_bounds__(K == 3 ? 576 : 256) void conv_wgrad_dma_kernel(
     const unsigned dy_bytes = (unsigned)((long long)h * w * dy.ld * 2), x_bytes = (unsigned)((long long)h * w * x.ld * 2);
     const unsigned lds0 = (unsigned)(unsigned long long)(__attribute__((address_space(3))) u32x4_t*)lds;
     auto issue = [&](long long u, int stage) {
-        const int tx = (int)(u % tiles_x);
-        const long long r = u / tiles_x;
-        const int ty = (int)(r % tiles_y), f = (int)(r / tiles_y);
+        // 32-bit unsigned (wave-uniform, scalar) division: the host checks n_units < 2^31
+        const unsigned uu = (unsigned)u, txs = (unsigned)tiles_x, tys = (unsigned)tiles_y;
+        const unsigned r = uu / txs;
+        const int tx = (int)(uu - r * txs);
+        const int f = (int)(r / tys), ty = (int)(r - (unsigned)f * tys);
         const int y0 = ty * WG_TH - 2, x0 = tx * WG_TW - 2;
         const T* dyf = img_ptr<T>(dy, f);
         const T* xf = img_ptr<T>(x, f);
@@ -1336,7 +1338,8 @@ extern "C" int dbsr_conv_wgrad_bias(int n_frames, int h, int w, dbsr_tensor x, i
     dd.c0 = 0;
     const dim3 grid(nbx, nty, ntz);
     // the LDS-DMA kernel (16-bit; buffer offsets of a frame within 31 bits), else the register-staged one
-    const bool dma = esz == 2 && (long long)h * w * std::max(x.ld, dy.ld) * 2 < (1LL << 31) && g_wgrad_dma;
+    const bool dma = esz == 2 && (long long)h * w * std::max(x.ld, dy.ld) * 2 < (1LL << 31) && units < (1LL << 31) &&
+                     g_wgrad_dma;
     int rc = by_dtype(x.dtype, [&](auto* tag) {
         using T = std::remove_pointer_t<decltype(tag)>;
 #define DBSR_WG(KK, CBB)                                                                                     \
