@@ -870,9 +870,10 @@ __global__ __launch_bounds__(256) void fuse_bwd_kernel(int B, int N, int hw, int
     const int groups = C / 8;
     const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= (long long)B * hw * groups) return;
-    const int g = (int)(idx % groups);
-    const long long pix = idx / groups;
-    const int b = (int)(pix / hw), rr = (int)(pix - (long long)b * hw);
+    // 32-bit index math (the host checks B * hw * groups < 2^31): 64-bit divisions cost ~100 VALU each
+    const unsigned ui = (unsigned)idx, pix = ui / (unsigned)groups;
+    const int g = (int)(ui - pix * (unsigned)groups);
+    const int b = (int)(pix / (unsigned)hw), rr = (int)(pix - (unsigned)b * (unsigned)hw);
     const int c = g * 8;
     float fu[8], dfu[8];
     load8(img_ptr<T>(fused, b) + (long long)rr * fused.ld + c, fu);
@@ -1579,6 +1580,7 @@ extern "C" int dbsr_fuse_backward(int B, int N, int hw, int c, dbsr_tensor weigh
     const dbsr_tensor* ts[] = {&weights, &ref, &fused, &dfused, &dlogits, &dref};
     for (auto* t : ts) DBSR_CHECK_ARG(t->dtype == ref.dtype && vec_ok(*t, 8), "fuse_backward: dtype/layout");
     const long long total = (long long)B * hw * (c / 8);
+    DBSR_CHECK_ARG(total < (1LL << 31), "fuse_backward: B * hw * c / 8 must be < 2^31");
     return by_dtype(ref.dtype, [&](auto* tag) {
         using T = std::remove_pointer_t<decltype(tag)>;
         hipLaunchKernelGGL((fuse_bwd_kernel<T>), dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, B, N, hw,
