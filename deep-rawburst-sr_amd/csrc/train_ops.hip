@@ -1042,7 +1042,7 @@ __global__ __launch_bounds__(256) void wb_count_kernel(int n, int h, int w, cons
     const int hw = h * w;
     const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= (long long)n * hw) return;
-    const int p = (int)(idx / hw), rr = (int)(idx - (long long)p * hw);
+    const int p = (int)((unsigned)idx / (unsigned)hw), rr = (int)((unsigned)idx - (unsigned)p * (unsigned)hw);   // n*hw < 2^31
     const float* fl = flow + (long long)p * fis;
     const WarpTaps t = warp_taps(rr % w, rr / w, w, h, fl[rr], fl[hw + rr]);
 #pragma unroll
@@ -1100,7 +1100,7 @@ __global__ __launch_bounds__(256) void wb_scatter_kernel(int n, int h, int w, co
     const int hw = h * w;
     const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= (long long)n * hw) return;
-    const int p = (int)(idx / hw), rr = (int)(idx - (long long)p * hw);
+    const int p = (int)((unsigned)idx / (unsigned)hw), rr = (int)((unsigned)idx - (unsigned)p * (unsigned)hw);   // n*hw < 2^31
     const float* fl = flow + (long long)p * fis;
     const WarpTaps t = warp_taps(rr % w, rr / w, w, h, fl[rr], fl[hw + rr]);
     int2* rec = records + (long long)p * 4 * hw;             // the pair's region: <= 4 records per pixel
@@ -1125,7 +1125,7 @@ __global__ __launch_bounds__(256) void wb_gather_kernel(int n, int h, int w, int
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const long long q = (long long)blockIdx.x * 4 + wv;
     if (q >= (long long)n * hw) return;
-    const int p = (int)(q / hw), rr = (int)(q - (long long)p * hw);
+    const int p = (int)((unsigned)q / (unsigned)hw), rr = (int)((unsigned)q - (unsigned)p * (unsigned)hw);   // n*hw < 2^31
     const int cnt = counts[q];
     const int2* rec = records + (long long)p * 4 * hw + offsets[q];
     const T* src = img_ptr<T>(dout, p);
@@ -1651,6 +1651,7 @@ extern "C" int dbsr_warp_backward_gather(int n, int h, int w, int c, dbsr_tensor
     DBSR_CHECK_ARG(n > 0 && h > 0 && w > 0 && c > 0 && c % 8 == 0 && vec_ok(dout, 8) && vec_ok(dfeat, 8) &&
                    (!gate.ptr || vec_ok(gate, 8)) && (long long)h * w * 4 < (1LL << 31),
                    "warp_backward_gather: c, ld and c0 must be multiples of 8");
+    DBSR_CHECK_ARG((long long)n * h * w < (1LL << 31), "warp_backward_gather: n * h * w must be < 2^31");
     DBSR_CHECK_ARG(workspace_bytes >= dbsr_warp_backward_gather_workspace_bytes(n, h, w),
                    "warp_backward_gather: workspace %zu < %zu bytes", workspace_bytes,
                    dbsr_warp_backward_gather_workspace_bytes(n, h, w));
