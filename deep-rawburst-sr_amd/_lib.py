@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get('DBSR_HIP_LIB', os.path.join(_HERE, 'libdbsr_hip.so'))
 DBSR_F32, DBSR_BF16, DBSR_F16 = 0, 1, 2
 ACT_NONE, ACT_RELU, ACT_LRELU = 0, 1, 2
 OUT_NHWC, OUT_SHUFFLE, OUT_NCHW_F32 = 0, 1, 2
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 
 class FrameMap(ctypes.Structure):
@@ -82,6 +82,7 @@ def lib():
             'dbsr_set_conv_algo': ([c_int], c_int),
             'dbsr_conv_kernel_for': ([ctypes.POINTER(ConvDesc)], c_int),
             'dbsr_conv_dispatch_variant': ([ctypes.POINTER(ConvDesc)], c_int),
+            'dbsr_conv_lane_reach': ([ctypes.POINTER(ConvDesc), c_int], c_int),
             'dbsr_conv_workspace_bytes': ([ctypes.POINTER(ConvDesc)], c_size_t),
             'dbsr_conv2d_head': ([ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_int, Tensor, c_void_p], c_int),
             'dbsr_conv_head_ok': ([ctypes.POINTER(ConvDesc)], c_int),
@@ -161,7 +162,7 @@ def lib():
 
 
 EXPORTED = ['dbsr_abi_version', 'dbsr_last_error', 'dbsr_conv_packed_elems', 'dbsr_conv_pack_weights', 'dbsr_conv2d',
-            'dbsr_set_conv_algo', 'dbsr_conv_kernel_for', 'dbsr_conv_dispatch_variant', 'dbsr_conv_workspace_bytes', 'dbsr_conv2d_head',
+            'dbsr_set_conv_algo', 'dbsr_conv_kernel_for', 'dbsr_conv_dispatch_variant', 'dbsr_conv_lane_reach', 'dbsr_conv_workspace_bytes', 'dbsr_conv2d_head',
             'dbsr_conv_head_ok',
             'dbsr_correlation', 'dbsr_correlation_backward', 'dbsr_backwarp', 'dbsr_warp_bilinear', 'dbsr_fuse_softmax',
             'dbsr_fuse_partial', 'dbsr_fuse_combine', 'dbsr_conv_fuse_softmax', 'dbsr_conv_fuse_ok',

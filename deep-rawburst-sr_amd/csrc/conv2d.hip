@@ -67,6 +67,21 @@ const dbsr_conv_desc* sel_view(const dbsr_conv_desc* d, dbsr_conv_desc& v) {
     return &v;
 }
 
+// The channel a lane's 16-B run of a residual / gate load starts at, for a cout tile whose lanes may lie past
+// cout (a partial tile): such lanes read the tile's first run instead (their values are never stored).  The
+// kernels address through these functions and the host reach model (conv_lane_reach, dbsr_conv_lane_reach)
+// enumerates the same lanes through them, so what the model checks is what the kernels load.
+// pipelined kernel: lane (h, g) of the cout tile at cb holds couts cb + 32h + 8g .. +7
+__host__ __device__ __forceinline__ int pipe_lane_ch(int cb, int h, int g, int cout) {
+    const int c = cb + 32 * h + 8 * g;
+    return c < cout ? c : cb;
+}
+// weight-stationary kernel: wave wc, lane group g of the cout tile at ctb holds couts ctb + 32wc + 8g .. +7
+__host__ __device__ __forceinline__ int ws_lane_ch(int ctb, int wc, int g, int cout) {
+    const int c = ctb + 32 * wc + 8 * g;
+    return c < cout ? c : ctb;
+}
+
 template <typename T> struct Frag;
 template <> struct Frag<bf16_t> {
     bf16x8_t v;
@@ -1023,8 +1038,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pipe_kernel(ConvK k, int tiles
 #pragma unroll
                 for (int q = 0; q < C::NOUT; ++q) {
                     const int h = q / C::GW, j = q % C::GW;
-                    const bool ok = t.cb + 32 * h + 8 * g < k.cout;
-                    gl[q] = *(const u32x4_t*)((const T*)k.gt + t.g_off + g_lane + grp_off(j) * k.g_ld + (ok ? 32 * h : 0));
+                    gl[q] = *(const u32x4_t*)((const T*)k.gt + t.g_off + g_lane + grp_off(j) * k.g_ld +
+                                              (pipe_lane_ch(t.cb, h, g, k.cout) - t.cb - 8 * g));
                 }
             }
         }
@@ -1129,16 +1144,14 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pipe_kernel(ConvK k, int tiles
                     if (fin) store_piece(q, prev);
                     if (has_res && last) {
                         const int h = q / C::GW, j = q % C::GW;
-                        const bool ok = cur.cb + 32 * h + 8 * g < k.cout;
                         resv[q] = *(const u32x4_t*)((const T*)k.r + cur.r_off + r_lane + grp_off(j) * k.r_ld +
-                                                    (ok ? 32 * h : 0));
+                                                    (pipe_lane_ch(cur.cb, h, g, k.cout) - cur.cb - 8 * g));
                     }
                     if constexpr (EPI == 0) {
                         if (has_gate && last) {
                             const int h = q / C::GW, j = q % C::GW;
-                            const bool ok = cur.cb + 32 * h + 8 * g < k.cout;
                             gatev[q] = *(const u32x4_t*)((const T*)k.gt + cur.g_off + g_lane + grp_off(j) * k.g_ld +
-                                                         (ok ? 32 * h : 0));
+                                                         (pipe_lane_ch(cur.cb, h, g, k.cout) - cur.cb - 8 * g));
                         }
                     }
                 }
@@ -1459,7 +1472,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ws_kernel(ConvK k, int tiles_x
             // cb itself can be >= cout, which at the last pixel of the last frame lies past the allocation)
 #pragma unroll
             for (int j = 0; j < C::GW; ++j)
-                gatev[j] = *(const u32x4_t*)((const T*)k.gt + t.g_off + px_off(j) * k.g_ld + (cout_ok ? 8 * g : -wc * 32));
+                gatev[j] = *(const u32x4_t*)((const T*)k.gt + t.g_off + px_off(j) * k.g_ld +
+                                             (ws_lane_ch(ct * WM, wc, g, k.cout) - cb));
         }
         const float4 b0 = *(const float4*)(lbias + wc * 32 + 8 * g);
         const float4 b1 = *(const float4*)(lbias + wc * 32 + 8 * g + 4);
@@ -2151,6 +2165,39 @@ int kernel_for(const dbsr_conv_desc* d) {
     return use_tiled(sel) ? 1 : 0;
 }
 
+// Host model of the highest channel of a pixel (c0 included) that any lane of the kernel dbsr_conv2d launches
+// for `d` touches in y (which 0), the residual (1) or the gate (2); -1 when that tensor is unused (or y is not
+// NHWC).  The pipelined and weight-stationary kernels address a partial cout tile's lanes through
+// pipe_lane_ch / ws_lane_ch, enumerated here over the last cout tile; the other kernels bound every element by
+// cout (epilogue_px's nvalid) and store only runs below cout; the weight-stationary residual arrives through a
+// buffer resource that spans its frame's ld-wide pixels, so a run past the last pixel lands zeros.
+int conv_lane_reach(const dbsr_conv_desc* d, int which) {
+    const dbsr_tensor& t = which == 0 ? d->y : which == 1 ? d->res : d->gate;
+    if (!t.ptr || d->out_mode != DBSR_OUT_NHWC) return -1;
+    dbsr_conv_desc v;
+    const dbsr_conv_desc* sel = sel_view(d, v);
+    const int kf = kernel_for(d);
+    int hi = d->cout - 1;
+    if (kf == 2 && which > 0) {
+        const int wm = pick_pipe(sel) == 2 ? 32 : 64;
+        const int cb = (d->cout - 1) / wm * wm;                 // the last, possibly partial, cout tile
+        for (int h = 0; h < wm / 32; ++h)
+            for (int g = 0; g < 4; ++g) hi = std::max(hi, pipe_lane_ch(cb, h, g, d->cout) + 7);
+    } else if (kf == 4 && which == 2) {
+        const int wm = ws_narrow(sel) ? 32 : 64;
+        const int ctb = (d->cout - 1) / wm * wm;
+        for (int wc = 0; wc < wm / 32; ++wc)
+            for (int g = 0; g < 4; ++g) hi = std::max(hi, ws_lane_ch(ctb, wc, g, d->cout) + 7);
+    } else if (kf == 4 && which == 1) {
+        return std::min(t.c0 + ((d->cout - 1) / 64 + 1) * 64 - 1, t.ld - 1);   // clamped by the frame's resource
+    }
+    return t.c0 + hi;
+}
+
+extern "C" int dbsr_conv_lane_reach(const dbsr_conv_desc* d, int which) {
+    return (d && which >= 0 && which <= 2) ? conv_lane_reach(d, which) : -2;
+}
+
 extern "C" int dbsr_conv_kernel_for(const dbsr_conv_desc* d) {
     return d ? kernel_for(d) : -1;
 }
@@ -2268,6 +2315,16 @@ extern "C" int dbsr_conv2d(const dbsr_conv_desc* d, void* stream) {
     if (d->gate.ptr)
         DBSR_CHECK_ARG(d->gate.dtype == d->y.dtype && d->gate.map.fpg > 0 && d->out_mode == DBSR_OUT_NHWC && !d->precise,
                        "conv2d: gate must be an NHWC tensor of the output dtype (NHWC output)");
+    // every lane's reads of the residual / gate and its stores stay inside the pixel's [c0, ld) slice, also for
+    // a partial cout tile at the last pixel of the last frame (where a run past ld would leave the allocation)
+    if (d->res.ptr) DBSR_CHECK_ARG(d->res.c0 + d->cout <= d->res.ld, "conv2d: residual slice exceeds ld");
+    if (d->gate.ptr) DBSR_CHECK_ARG(d->gate.c0 + d->cout <= d->gate.ld, "conv2d: gate slice exceeds ld");
+    for (int w = 0; w < 3; ++w) {
+        const dbsr_tensor& t = w == 0 ? d->y : w == 1 ? d->res : d->gate;
+        const int reach = conv_lane_reach(d, w);
+        DBSR_CHECK_ARG(reach < t.ld, "conv2d: a lane of the %s would address channel %d of a %d-channel pixel",
+                       w == 0 ? "output" : w == 1 ? "residual" : "gate", reach, t.ld);
+    }
     const long long npix = (long long)d->n_frames * d->out_h * d->out_w;
     DBSR_CHECK_ARG(npix < (1LL << 31), "conv2d: too many pixels");
 

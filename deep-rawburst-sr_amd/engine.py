@@ -615,10 +615,10 @@ class DBSREngine:
     FUSED_HEAD = True
     # weight-predictor input conv split into a per-frame [proj, offfeat] conv + a per-burst base conv
     LINEAR_SPLIT = True
-    # weight-predictor output conv + softmax + fusion in one kernel (dbsr_conv_fuse_softmax: the logits never
-    # reach memory).  Off: measured 468-563 us per cfg2 step against 407 us for dbsr_conv2d (pipelined) +
-    # dbsr_fuse_softmax -- one wave per SIMD exposes the per-frame epilogue and latencies
-    FUSED_WP_OUT = False
+    # weight-predictor output conv + softmax + fusion in one kernel (dbsr_conv_fuse_softmax: the fp32 logits never
+    # reach memory) wherever the library serves the shape (16-bit, N = 14, cout % 128 == 0);
+    # otherwise dbsr_conv2d into a logits buffer + dbsr_fuse_softmax
+    FUSED_WP_OUT = True
 
     def __init__(self, net):
         self.net = net

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define DBSR_ABI_VERSION 14
+#define DBSR_ABI_VERSION 15
 
 enum { DBSR_F32 = 0, DBSR_BF16 = 1, DBSR_F16 = 2 };
 enum { DBSR_ACT_NONE = 0, DBSR_ACT_RELU = 1, DBSR_ACT_LRELU = 2 };      /* LeakyReLU slope 0.1 */
@@ -126,6 +126,12 @@ int dbsr_conv_kernel_for(const dbsr_conv_desc* d);
  * tile*1000 + K split; precise: pixel tile).  Two descs with equal variants sum every output in the same
  * order (the frame-sharding tests compare a slab's variants with the whole image's). */
 int dbsr_conv_dispatch_variant(const dbsr_conv_desc* d);
+/* Host model of the highest channel of a pixel (c0 included) that any lane of the kernel dbsr_conv2d would
+ * launch for `d` touches in y (which 0: stores), the residual (1) or the gate (2) -- including the lanes of a
+ * partial cout tile past cout, which the pipelined and weight-stationary kernels point at their tile's first
+ * run; -1 when that tensor is unused or y is not NHWC; -2 on a bad argument.  dbsr_conv2d returns DBSR_E_ARG
+ * when it is >= the tensor's ld (a run past the last pixel of the last frame would leave the allocation). */
+int dbsr_conv_lane_reach(const dbsr_conv_desc* d, int which);
 /* A 32-channel ResBlock conv2 fused with a 1x1 head (the decoder's last post-ResBlock + RGB predictor,
  * decoders.py:59-61 / blocks.py:94-96): t = ReLU(conv(x) + bias + residual) stays in registers (d->y is
  * not written) and out = ReLU(head_w . t + head_b) is stored fp32 NCHW (head_out.img_stride =
@@ -170,12 +176,15 @@ int dbsr_fuse_softmax(int B, int N, int hw, int c, dbsr_tensor logits, dbsr_tens
                       dbsr_tensor fused, dbsr_tensor weights, void* stream);
 
 /* The weight predictor's last conv fused with the softmax over the burst and the weighted sum
- * (models/dbsr/merging.py:55-57,113-124): logits = conv(d) for the B*N frames of
- * d->x (frame b*N+n of burst b) never reach memory -- each (burst, 16x4 tile, 64 channels) block keeps
- * all N frames' logits (rounded to the conv dtype, as dbsr_conv2d would store them) in registers.
- * ref / oth / fused / weights address as in dbsr_fuse_softmax (c = d->cout); d->y, d->res are unused.
- * Requires dbsr_conv_fuse_ok(d, B, N): 16-bit 3x3/s1/p1/d1, cin_pad 64 or 128, cout % 64 == 0,
- * d->n_frames == B*N, N == 14, width % 16 == 0, height % 4 == 0. */
+ * (models/dbsr/merging.py:55-57,113-124): logits = conv(d) + bias for the B*N frames
+ * of d->x (frame b*N+n of burst b) never reach memory and are never rounded -- each (burst, 16x2 pixels,
+ * 128 channels) super-tile keeps all N frames' fp32 logits in its waves' accumulators; weights = softmax over
+ * the N frames (fp32, stored in the conv dtype), fused = sum_n weights * features (fp32, stored in the dtype).
+ * ref / oth / fused / weights address as in dbsr_fuse_softmax (c = d->cout; weights.ptr NULL: no aux output);
+ * d->y, d->res are unused; d->max_blocks caps the persistent grid.  Requires dbsr_conv_fuse_ok(d, B, N):
+ * 16-bit 3x3/s1/p1/d1, cin > 16, cout % 128 == 0 (<= 512), d->n_frames == B*N, N == 14, width % 16 == 0,
+ * height % 2 == 0, and frame maps affine in (burst, frame); the feature / output tensors need ld and c0
+ * multiples of 8 with c0 + cout <= ld (DBSR_E_ARG otherwise). */
 int dbsr_conv_fuse_softmax(const dbsr_conv_desc* d, int B, int N, dbsr_tensor ref, dbsr_tensor oth,
                            dbsr_tensor fused, dbsr_tensor weights, void* stream);
 int dbsr_conv_fuse_ok(const dbsr_conv_desc* d, int B, int N);
@@ -298,7 +307,8 @@ int dbsr_conv_wgrad(int n_frames, int h, int w, dbsr_tensor x, int cin, dbsr_ten
  * (torch.nn.grad.conv2d_weight + grad_output.sum((0, 2, 3)), which the reference's training step gets from
  * autograd: actors/dbsr_actors.py:27-47).  Same workspace as dbsr_conv_wgrad. */
 /* Which wgrad kernel 16-bit dbsr_conv_wgrad(_bias) runs: 1 (default) the LDS-DMA ring kernel, 0 the register-
- * staged one (fp32 always runs the latter).  Both sum in the same order: results are bitwise equal. */
+ * staged one (fp32 always runs the latter).  Both sum dw in the same order (bitwise equal); db is equal up to
+ * fp32 summation order (the ring kernel sums it from the dY fragments of its tap-5 wave). */
 int dbsr_set_wgrad_algo(int algo);
 int dbsr_conv_wgrad_bias(int n_frames, int h, int w, dbsr_tensor x, int cin, dbsr_tensor dy, int cout, int k,
                          float* dw, float* db, int accumulate, void* workspace, size_t workspace_bytes, void* stream);

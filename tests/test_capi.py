@@ -248,3 +248,62 @@ def test_plan_h_misfit_rejected(L):
     d.x.ptr, d.y.ptr = 16, 16
     assert lib.dbsr_conv2d(d, None) == -1
     assert b'plan_h' in lib.dbsr_last_error()
+
+
+def _tight_conv(L, n, h, w, cin, cout, res=False, gate=False):
+    """A 16-bit 3x3 conv whose output / residual / gate are tight NHWC tensors (ld == cout, c0 == 0): a lane run
+    past cout at the last pixel of the last frame would leave the allocation."""
+    d = L.ConvDesc()
+    d.n_frames = n
+    d.x = L.Tensor(1, L.DBSR_BF16, h * w * cin, cin, 0, L.FrameMap(1, 1, 0, 1))
+    d.in_h, d.in_w, d.out_h, d.out_w = h, w, h, w
+    d.cin, d.cout, d.kh, d.kw, d.stride, d.pad, d.dil = cin, cout, 3, 3, 1, 1, 1
+    d.w = 1
+    t = lambda: L.Tensor(1, L.DBSR_BF16, h * w * cout, cout, 0, L.FrameMap(1, 1, 0, 1))   # noqa: E731
+    d.y = t()
+    d.act = L.ACT_NONE if res else L.ACT_RELU
+    d.res = t() if res else L.NULL_TENSOR
+    d.post_act = L.ACT_RELU if res else L.ACT_NONE
+    d.gate = t() if gate else L.NULL_TENSOR
+    return d
+
+
+@pytest.mark.parametrize('case', [
+    # (frames, h, w, cin, cout, residual, gate, expected kernel): partial cout tiles of the pipelined kernel
+    # (64-cout tiles: 80, 96; 32-cout tiles: 24) and of the weight-stationary kernel (64: 80, 40; 32: 24)
+    (112, 48, 48, 128, 80, True, False, 2), (112, 48, 48, 128, 96, False, True, 2), (112, 48, 48, 128, 80, True, True, 2),
+    (8, 128, 128, 64, 24, True, True, 2), (112, 48, 48, 64, 80, False, True, 4), (112, 48, 48, 64, 40, True, True, 4),
+    (8, 128, 128, 32, 24, True, True, 4)])
+def test_partial_cout_lanes_stay_in_pixel(L, case):
+    """VERDICT r4 #5 (the 16-B read past the gate tensor of 390f678): the host model of the lanes' channel
+    addressing (dbsr_conv_lane_reach, enumerating the kernels' own pipe_lane_ch / ws_lane_ch) keeps every
+    residual / gate read and every store of the last, partial cout tile inside the pixel, for tight tensors."""
+    n, h, w, cin, cout, res, gate, kern = case
+    lib = L.lib()
+    d = _tight_conv(L, n, h, w, cin, cout, res, gate)
+    assert lib.dbsr_conv_kernel_for(d) == kern
+    wm = 32 if cout <= 32 else 64
+    assert (cout - 1) // wm * wm + wm > cout            # the case has a partial cout tile
+    for which, on in ((0, True), (1, res), (2, gate)):
+        r = lib.dbsr_conv_lane_reach(d, which)
+        if on:
+            assert 0 <= r <= cout - 1, (which, r)
+        else:
+            assert r == -1
+    assert lib.dbsr_conv_lane_reach(d, 3) == -2
+
+
+def test_conv_rejects_slices_past_ld(L):
+    """A residual / gate slice that does not fit its pixel (c0 + cout > ld) is an argument error, before any
+    launch."""
+    lib = L.lib()
+    d = _tight_conv(L, 112, 48, 48, 128, 80, res=True)
+    d.x.ptr = d.y.ptr = d.res.ptr = 1 << 20
+    d.res.c0 = 8
+    assert lib.dbsr_conv2d(d, None) == -1
+    assert b'residual slice exceeds ld' in lib.dbsr_last_error()
+    d = _tight_conv(L, 112, 48, 48, 64, 80, gate=True)
+    d.x.ptr = d.y.ptr = d.gate.ptr = 1 << 20
+    d.gate.ld = 72
+    assert lib.dbsr_conv2d(d, None) == -1
+    assert b'gate slice exceeds ld' in lib.dbsr_last_error()

@@ -1,13 +1,13 @@
 """dbsr_conv_fuse_softmax (the weight predictor's last conv + softmax over the
-burst + fusion in one kernel, models/dbsr/merging.py:55-57,113-124) against torch on the same 16-bit
-operands, and against the two-kernel path (dbsr_conv2d to a logits buffer + dbsr_fuse_softmax).
+burst + fusion in one kernel, models/dbsr/merging.py:55-57,113-124; the product default,
+DBSREngine.FUSED_WP_OUT) against torch on the same 16-bit operands, and against the two-kernel path
+(dbsr_conv2d to a 16-bit logits buffer + dbsr_fuse_softmax).
 
-Tolerances: the logits are rounded to the compute dtype as the two-kernel path stores them, but their
-K sum runs in two halves (the kernel's waves split K) and the softmax statistics accumulate online, so
-against the two-kernel path >= 99 % of weights / fused values agree to 1 ulp of the output dtype and
-all within the torch tolerance below.
-Against torch (fp32 conv of the rounded operands, fp32 softmax): weights atol 2e-3 + rtol 5e-2, fused
-atol 2e-2 (a logit that lands on the other side of a 16-bit rounding boundary moves its weight)."""
+Tolerances.  Against torch (fp32 conv of the rounded operands + bias, fp32 softmax, fp32 weighted sum --
+the kernel's own arithmetic, the logits never rounded): the outputs differ by the K summation order and the
+final rounding to the 16-bit output dtype: weights atol 1e-3 + rtol 1e-2 of the dtype, fused atol 1e-2.
+Against the two-kernel path, which rounds every logit to 16 bits before the softmax: a weight moves by up
+to |l| * 2^-8 (bf16) / 2^-11 (fp16) relative, so rtol 5e-2 (bf16) / 1e-2 (fp16) at the |l| <~ 6 here."""
 import ctypes
 
 import numpy as np
@@ -16,26 +16,7 @@ import torch
 import torch.nn.functional as F
 
 DEV = 'cuda'
-
-
-def _experimental_built():
-    """The fused kernel is measured slower and ships only in an experimental build (-DDBSR_EXPERIMENTAL=1,
-    loaded through DBSR_HIP_LIB)."""
-    try:
-        from dbsr_amd import _lib as L
-        d = L.ConvDesc()
-        d.n_frames = 28
-        d.x = L.Tensor(1, L.DBSR_BF16, 48 * 48 * 128, 128, 0, L.FrameMap(1, 1, 0, 1))
-        d.in_h = d.in_w = d.out_h = d.out_w = 48
-        d.cin, d.cout, d.kh, d.kw, d.stride, d.pad, d.dil = 128, 512, 3, 3, 1, 1, 1
-        d.w = 1
-        return bool(L.lib().dbsr_conv_fuse_ok(ctypes.byref(d), 2, 14))
-    except Exception:
-        return False
-
-
-pytestmark = [pytest.mark.gpu,
-              pytest.mark.skipif(not _experimental_built(), reason='experimental conv_fuse kernel not built')]
+pytestmark = pytest.mark.gpu
 
 
 def _case(B, N, H, W, cin, C, dt, seed, want_fw=True):
@@ -76,50 +57,45 @@ def _case(B, N, H, W, cin, C, dt, seed, want_fw=True):
         plan.run(s)
         torch.cuda.synchronize()
         outs[fused_path] = (FUS.t.float().cpu(), FW.t.float().cpu())
-    # torch reference on the rounded operands; logits rounded like the stored ones
+    # torch reference on the rounded operands, fp32 logits (as the fused kernel keeps them)
     hb = h.to(dt).float()
     wb = w_cpu.to(dt).float()
-    lg = F.conv2d(hb, wb, b_cpu, padding=1).to(dt).float().reshape(B, N, C, H, W)
+    lg = F.conv2d(hb, wb, b_cpu, padding=1).reshape(B, N, C, H, W)
     wts = torch.softmax(lg, dim=1)
     fz = (feat.to(dt).float() * wts).sum(dim=1)
     ref = (fz.permute(0, 2, 3, 1), wts.reshape(B * N, C, H, W).permute(0, 2, 3, 1))
     return outs, ref
 
 
-def _ulp_close(a, b, dt, atol=2e-3):
-    """<= 1 ulp of the output dtype (bf16 <= 2^-7, fp16 <= 2^-10 relative) on >= 99 % of the values;
-    the rest within the torch tolerance (a logit summed in another order can round to the neighbouring
-    16-bit value, which moves its weight by up to |l| * ulp)."""
-    eps = 2.0 ** -7 if dt == torch.bfloat16 else 2.0 ** -10
-    bad = (a - b).abs() > eps * torch.maximum(a.abs(), b.abs()) + 1e-6
-    frac = bad.float().mean().item()
-    assert frac <= 1e-2, '%d of %d beyond 1 ulp' % (int(bad.sum()), bad.numel())
-    np.testing.assert_allclose(a.numpy(), b.numpy(), atol=atol, rtol=5e-2)
-
-
 @pytest.mark.parametrize('case', [(2, 14, 48, 48, 128, 512, torch.bfloat16),    # the bench shape's layer
-                                  (1, 14, 32, 16, 128, 128, torch.float16),     # fp16, non-square
-                                  (3, 14, 8, 48, 128, 192, torch.bfloat16)])    # 3 channel slices
-def test_conv_fuse_vs_two_kernel_and_torch(case):
+                                  (2, 14, 48, 48, 128, 512, torch.float16),     # ... at the bench dtype
+                                  (1, 14, 32, 16, 128, 128, torch.float16),     # non-square, one channel slice
+                                  (3, 14, 8, 48, 96, 256, torch.bfloat16)])     # 3 input chunks, 2 slices
+def test_conv_fuse_vs_torch_and_two_kernel(case):
     B, N, H, W, cin, C, dt = case
     outs, (rf, rw) = _case(B, N, H, W, cin, C, dt, seed=B * 100 + H + C)
     (f1, w1), (f0, w0) = outs[True], outs[False]
-    _ulp_close(w1, w0, dt)
-    _ulp_close(f1, f0, dt, atol=2e-2)
-    # a logit l rounded to the other side of a 16-bit boundary than torch's moves its weight by up to
-    # |l| * 2^-8 (bf16) relative: rtol 5e-2 at the |l| <~ 6 of these cases
-    np.testing.assert_allclose(w1.numpy(), rw.numpy(), atol=2e-3, rtol=5e-2)
-    np.testing.assert_allclose(f1.numpy(), rf.numpy(), atol=2e-2, rtol=1e-2)
+    eps = 2.0 ** -8 if dt == torch.bfloat16 else 2.0 ** -11
+    # against torch: summation order + one rounding of each output to the dtype
+    np.testing.assert_allclose(w1.numpy(), rw.numpy(), atol=1e-3, rtol=2 * eps)
+    np.testing.assert_allclose(f1.numpy(), rf.numpy(), atol=1e-2, rtol=4 * eps)
+    # against the two-kernel path: its logits are rounded to the dtype first (bf16: a weight moves by up to
+    # |l| * 2^-8 relative, a fused value by the sum of those over the burst -- measured up to 0.047 here)
+    rt = 5e-2 if dt == torch.bfloat16 else 1e-2
+    np.testing.assert_allclose(w1.numpy(), w0.numpy(), atol=2e-3, rtol=rt)
+    np.testing.assert_allclose(f1.numpy(), f0.numpy(), atol=8e-2 if dt == torch.bfloat16 else 2e-2, rtol=rt)
+    # the fused kernel is closer to torch than the two-kernel path (the logits are not rounded)
+    assert (w1 - rw).abs().mean() <= (w0 - rw).abs().mean()
     # the weights of a pixel sum to 1 over the burst
     s = w1.reshape(B, N, H, W, C).sum(dim=1)
     assert (s - 1).abs().max() < 0.05
 
 
 def test_conv_fuse_without_aux_weights():
-    outs, (rf, _) = _case(1, 14, 16, 48, 128, 64, torch.bfloat16, seed=7, want_fw=False)
+    outs, (rf, _) = _case(1, 14, 16, 48, 128, 128, torch.bfloat16, seed=7, want_fw=False)
     f1, w1 = outs[True]
     assert w1.abs().max() == 0                   # aux output skipped
-    np.testing.assert_allclose(f1.numpy(), rf.numpy(), atol=2e-2, rtol=1e-2)
+    np.testing.assert_allclose(f1.numpy(), rf.numpy(), atol=1e-2, rtol=2 ** -6)
 
 
 def test_conv_fuse_rejects_unsupported():
@@ -133,6 +109,12 @@ def test_conv_fuse_rejects_unsupported():
     assert L.lib().dbsr_conv_fuse_ok(ctypes.byref(d), 2, 13) == 0          # burst size 13
     d.n_frames = 28
     assert L.lib().dbsr_conv_fuse_ok(ctypes.byref(d), 2, 14) == 1
+    d.cout = 192
+    assert L.lib().dbsr_conv_fuse_ok(ctypes.byref(d), 2, 14) == 0          # cout % 128
+    d.cout = 512
+    d.in_h = d.out_h = 47
+    assert L.lib().dbsr_conv_fuse_ok(ctypes.byref(d), 2, 14) == 0          # odd height
+    d.in_h = d.out_h = 48
     d.x.dtype = L.DBSR_F32
     assert L.lib().dbsr_conv_fuse_ok(ctypes.byref(d), 2, 14) == 0          # fp32: two-kernel path
 
