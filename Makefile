@@ -27,6 +27,11 @@ $(OBJDIR)/%.o: $(SRC)/%.cpp include/dbsr_hip.h
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(FLAGS) -c $< -o $@
 
+# No SLP vectorisation for the fused weight-predictor kernel: ROCm 7.2's gfx950 code emitted a packed-fp32
+# v_pk_mul_f32 that overwrote a 16-B buffer store's data registers right after the store, and the store wrote
+# the new values for part of the wave; scalar fp32 ops are also the cheaper ones beside MFMAs.
+$(OBJDIR)/conv_fuse.o: FLAGS += -fno-slp-vectorize
+
 $(LIB): $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
 

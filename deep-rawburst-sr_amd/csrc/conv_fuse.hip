@@ -71,6 +71,20 @@ struct StaticFor {
     }
 };
 
+// One 1-KiB LDS-DMA piece issued from inline asm (as conv_wgrad_dma_kernel does): the compiler's wait insertion
+// does not see it, so it neither drains every outstanding piece before the fragment reads (it cannot tell the
+// ring stage being read from the stages being filled) nor at every __syncthreads; the kernel counts its own
+// pieces (vmcnt is in order, so the compiler's own waits only get stricter).  rsrc words: base, stride 0,
+// num_records, raw-buffer flags.
+__device__ __forceinline__ void fz_dma(const void* base, unsigned bytes, int voff, int soff, unsigned lds_addr) {
+    const unsigned long long a = (unsigned long long)base;
+    typedef int i32x4_t __attribute__((ext_vector_type(4)));
+    const i32x4_t r = {(int)(unsigned)a, (int)((unsigned)(a >> 32) & 0xffffu), (int)bytes, 0x00020000};
+    asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, %3 offen lds" ::"v"(voff), "s"(r), "s"(lds_addr),
+                 "s"(soff)
+                 : "memory", "m0");
+}
+
 // pixel-major halo image of one 32-channel chunk: halo pixel p's 4 k-groups at slots 4p..4p+3, k-group g
 // at 4p + phys(p, g) (the pipelined conv kernel's swizzle: conflict-free ds_read_b128 for every tap shift)
 __device__ __forceinline__ int halo_phys(int p, int g) { return 2 * (g & 1) + ((g >> 1) ^ ((p >> 2) & 1)); }
@@ -86,22 +100,29 @@ struct FuseK {
     const void* oth; long long oth_b, oth_n; int oth_ld;   // frame n >= 1: oth + b*oth_b + (n-1)*oth_n
     void* fused; long long fus_b; int fus_ld;
     void* wts; long long wts_b, wts_n; int wts_ld;         // aux fusion weights (nullptr: not written)
+    // the epilogue's loads / stores go through a buffer resource per (tensor, burst): byte spans of a burst's
+    // frames (< 2^31, checked on the host) and per-frame byte strides (wave-uniform soffset)
+    unsigned ref_span, oth_span, wts_span;
+    int oth_nb, wts_nb;
 };
 
 template <int NF>
 struct FuseCfg {
     static constexpr int WM = 128, TW = 16, TH = 2, NWAVES = 8;
-    static constexpr int HWD = TW + 2;                        // halo row width
-    static constexpr int HPX = TH * HWD;                      // halo pixels per (frame, kernel row): 36
-    static constexpr int HP = (HPX + 15) / 16;                // 1-KiB pieces per (frame, kernel row): 3
+    static constexpr int HWD = TW + 2;                        // input row width of a tile: 18
+    static constexpr int ROW_PX = NF * HWD;                   // one input row of the burst's N frames: 252
+    static constexpr int RP = (ROW_PX + 15) / 16;             // its 1-KiB pieces (16 pixels x 4 k-groups): 16
+    static constexpr int NROW = 5;                            // row ring slots
     static constexpr int W_ITEMS = 3 * (WM / 16);             // weight pieces per stage: (tap, 16-cout block)
-    static constexpr int IN_ITEMS = NF * HP;
-    static constexpr int ITEMS = W_ITEMS + IN_ITEMS;          // 66 at N = 14
-    static constexpr int PER = (ITEMS + NWAVES - 1) / NWAVES; // DMA pieces per wave per stage (uniform)
-    static constexpr int STAGE_U4 = ITEMS * 64;               // 16-B slots per stage buffer
-    static constexpr int BIAS_U4 = 512 / 4;                   // cout <= 512 fp32 biases
-    static constexpr int LDS_U4 = 2 * STAGE_U4 + BIAS_U4;
-    static_assert(LDS_U4 * 16 <= 160 * 1024, "two stage buffers + bias must fit the LDS");
+    static constexpr int NWB = 3;                             // weight ring buffers
+    static constexpr int W_U4 = W_ITEMS * 64, ROW_U4 = RP * 64;
+    static constexpr int ROWS_OFF = NWB * W_U4;               // row ring after the weight ring
+    static constexpr int BIAS_OFF = ROWS_OFF + NROW * ROW_U4;
+    static constexpr int LDS_U4 = BIAS_OFF + 512 / 4;         // + cout <= 512 fp32 biases
+    static constexpr int PER1 = (W_ITEMS + RP) / NWAVES;      // DMA pieces per wave for a stage with one new row
+    static constexpr int PER2 = (W_ITEMS + 2 * RP) / NWAVES;  // ... with two (kernel row 0 of a chunk)
+    static_assert((W_ITEMS + RP) % NWAVES == 0 && (W_ITEMS + 2 * RP) % NWAVES == 0, "whole pieces per wave");
+    static_assert(LDS_U4 * 16 <= 160 * 1024, "weight ring + row ring + bias must fit the LDS");
 };
 
 template <typename T, int NF>
@@ -109,7 +130,7 @@ __global__ __launch_bounds__(512, 1) void conv_fuse_kernel(FuseK k, int tiles_x,
     using C = FuseCfg<NF>;
     DBSR_OWN_SIMDS();
     __shared__ __attribute__((aligned(16))) u32x4_t lds[C::LDS_U4];
-    float* lbias = (float*)(lds + 2 * C::STAGE_U4);
+    float* lbias = (float*)(lds + C::BIAS_OFF);
 
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int g = lane >> 4, col = lane & 15;
@@ -136,45 +157,52 @@ __global__ __launch_bounds__(512, 1) void conv_fuse_kernel(FuseK k, int tiles_x,
         return t;
     };
 
-    // one 1-KiB DMA piece of stage (super-tile t, chunk c, kernel row ky): piece `it` of this wave is item
-    // wave + 8*it of the stage image (clamped: surplus slots re-issue the last piece, an identical write).
-    // Items [0, W_ITEMS): weights of tap 3ky + kx, 16-cout block b (contiguous 1 KiB of the packed copy);
-    // then frame n's input rows in pieces of 16 halo pixels x 4 k-groups (lane -> pixel, physical slot).
+    // The LDS holds a 3-buffer ring of stage weights and a 5-slot ring of input rows, and the pieces of stage
+    // s + 2 are issued during stage s (two stages in flight: the LDS-DMA latency, not the MFMAs, bounded the
+    // double-buffered version).  Stage (chunk c, kernel row ky) reads input rows ky, ky + 1 of the chunk's 4
+    // (tile rows y0 - 1 .. y0 + 2); each row, with all N frames' 18 pixels, is loaded once per chunk: 2 new rows
+    // for ky = 0, one for ky = 1, 2.  Row r of global chunk number gc lives in slot (4 gc + r) % 5, which no
+    // stage in flight still reads.
+    // One 1-KiB DMA piece of stage (super-tile t, chunk c, kernel row ky, global chunk gc) into weight buffer wb:
+    // piece `it` of this wave is item wave + 8*it; items [0, W_ITEMS): weights of tap 3ky + kx, 16-cout block b
+    // (contiguous 1 KiB of the packed copy); then the new rows' pieces of 16 row pixels x 4 k-groups (lane ->
+    // frame n = p / 18, column p % 18, physical slot).
     const int pix_b = k.x_ld * (int)sizeof(T);
-    const __amdgpu_buffer_rsrc_t w_rsrc = buf_rsrc(k.w_pipe, 0xffffffffu);
+    const unsigned lds0 = (unsigned)(unsigned long long)(__attribute__((address_space(3))) u32x4_t*)lds;
     // one buffer resource over the burst's N input frames (x_span bytes < 2^31, checked on the host): an
-    // out-of-frame halo pixel gets voffset BUF_OOB, past num_records, and lands zeros
-    auto dma = [&](int it, const Tile& t, int c, int ky, int buf) {
-        const int item = min(wave + C::NWAVES * it, C::ITEMS - 1);
-        u32x4_t* dst = lds + buf * C::STAGE_U4 + item * 64;
+    // out-of-frame pixel gets voffset BUF_OOB, past num_records, and lands zeros
+    auto dma = [&](int it, const Tile& t, int c, int ky, int gc, int wb) {
+        const int item = wave + C::NWAVES * it;
         if ((DBSR_FUSE_ABL & 4) && item < C::W_ITEMS) return;   // (timing only)
         if ((DBSR_FUSE_ABL & 2) && item >= C::W_ITEMS) return;
         if (item < C::W_ITEMS) {
             const int kx = item / (C::WM / 16), b16 = item % (C::WM / 16);
             const int piece = (((t.cb >> 4) + b16) * k.nchunks + c) * 9 + 3 * ky + kx;
-            blds16(w_rsrc, lane * 16, piece * 1024, dst);
+            fz_dma(k.w_pipe, 0xffffffffu, lane * 16, piece * 1024, lds0 + (wb * C::W_U4 + item * 64) * 16);
         } else {
-            const int hi = item - C::W_ITEMS;
-            const int n = hi / C::HP, j = hi - n * C::HP;
+            const int ri = item - C::W_ITEMS;
+            const int r = (ky == 0 ? 0 : ky + 1) + ri / C::RP, j = ri % C::RP;
+            const int slot = (4 * gc + r) % C::NROW;
             int ln = lane;
             asm volatile("" : "+v"(ln));        // keep the lane math here (not hoisted into spilled registers)
             const int p = 16 * j + (ln >> 2), ph = ln & 3;
             const int gg = 2 * ((ph & 1) ^ ((p >> 2) & 1)) + (ph >> 1);
-            const int r = p >= C::HWD ? 1 : 0, cc = p - r * C::HWD;
-            const int hy = t.y0 - 1 + ky + r, hx = t.x0 - 1 + cc;
-            const bool ok = p < C::HPX && (unsigned)hy < (unsigned)k.H && (unsigned)hx < (unsigned)k.W;
-            const T* xb = (const T*)k.x + t.bb * k.x_b;
-            blds16(buf_rsrc(xb, k.x_span), ok ? n * k.x_nb + (hy * k.W + hx) * pix_b + c * 64 + gg * 16 : BUF_OOB, 0,
-                   dst);
+            const int n = p / C::HWD, cc = p - n * C::HWD;
+            const int hy = t.y0 - 1 + r, hx = t.x0 - 1 + cc;
+            const bool ok = p < C::ROW_PX && (unsigned)hy < (unsigned)k.H && (unsigned)hx < (unsigned)k.W;
+            fz_dma((const T*)k.x + t.bb * k.x_b, k.x_span,
+                   ok ? n * k.x_nb + (hy * k.W + hx) * pix_b + c * 64 + gg * 16 : BUF_OOB, 0,
+                   lds0 + (C::ROWS_OFF + slot * C::ROW_U4 + j * 64) * 16);
         }
     };
 
-    // lane-dependent LDS bases: B-fragment of tap kx = halo pixel wr*18 + col + kx, k-group g; A-fragment of
-    // 16-cout block (2wc + i) at tap kx = weight item kx*8 + 2wc + i, row col, k-group g
-    const int P0 = wr * C::HWD + col;
-    int in_base[3];
+    // lane-dependent LDS bases: the B-fragment of frame n at tap kx reads row pixel m = 18n + kx + col of the
+    // row slot, k-group g: slot 4(m + col) + halo_phys(m + col, g), where halo_phys depends on m only through
+    // m & 7 (8 per-lane bases + an immediate 4m); the A-fragment of 16-cout block (2wc + i) at tap kx is weight
+    // item kx*8 + 2wc + i, row col, k-group g
+    int base8[8];
 #pragma unroll
-    for (int kx = 0; kx < 3; ++kx) in_base[kx] = 4 * (P0 + kx) + halo_phys(P0 + kx, g);
+    for (int rho = 0; rho < 8; ++rho) base8[rho] = 4 * col + halo_phys(col + rho, g);
     const int a_base = 2 * wc * 64 + g * 16 + col;
 
     f32x4_t acc[NF][2];
@@ -184,31 +212,40 @@ __global__ __launch_bounds__(512, 1) void conv_fuse_kernel(FuseK k, int tiles_x,
     // (y0 + wr, x0 + col): acc[n][0] = couts ch..ch+3, acc[n][1] = ch+4..ch+7
     auto lane_pix = [&](const Tile& t) { return (t.y0 + wr) * k.W + t.x0 + col; };
     auto lane_ch = [&](const Tile& t) { return t.cb + 32 * wc + 8 * g; };
-    // (a wave-uniform frame base + a 32-bit lane byte offset: the scalar-base addressing form)
+    // (buffer loads / stores: a per-(tensor, burst) resource, the lane's 32-bit byte offset -- the same for every
+    // frame -- and the frame's uniform byte offset as soffset; no per-frame 64-bit lane addresses in registers)
     auto feat_load = [&](const Tile& t, int n, u32x4_t& dst) {
         const unsigned pix = lane_pix(t), ch = lane_ch(t);
-        const char* fb = n == 0 ? (const char*)((const T*)k.ref + t.bb * k.ref_b)
-                                : (const char*)((const T*)k.oth + t.bb * k.oth_b + (n - 1) * k.oth_n);
-        const unsigned off = (pix * (unsigned)(n == 0 ? k.ref_ld : k.oth_ld) + ch) * (unsigned)sizeof(T);
-        dst = __builtin_nontemporal_load((const u32x4_t*)(fb + off));
+        if (n == 0) {
+            const auto r = buf_rsrc((const T*)k.ref + t.bb * k.ref_b, k.ref_span);
+            dst = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
+                r, (int)((pix * (unsigned)k.ref_ld + ch) * (unsigned)sizeof(T)), 0, 2));
+        } else {
+            const auto r = buf_rsrc((const T*)k.oth + t.bb * k.oth_b, k.oth_span);
+            dst = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
+                r, (int)((pix * (unsigned)k.oth_ld + ch) * (unsigned)sizeof(T)), (n - 1) * k.oth_nb, 2));
+        }
     };
+    // The weights go out as global stores: ROCm 7.2 pads a VALU write of a global store's data registers right
+    // after the store with the wait states gfx950 needs, but not after the buffer-store builtin, where the store
+    // then wrote the overwritten values for part of the wave.  The lane offset passes an empty asm
+    // inside the epilogue, so the per-frame 64-bit addresses are formed there and not hoisted out of the stage loop.
     auto store_w = [&](const Tile& t, int n, const u32x4_t& v) {
         if (k.wts) {
-            const unsigned off = ((unsigned)lane_pix(t) * (unsigned)k.wts_ld + (unsigned)lane_ch(t)) * (unsigned)sizeof(T);
-            char* fb = (char*)((T*)k.wts + t.bb * k.wts_b + n * k.wts_n);
+            unsigned off = ((unsigned)lane_pix(t) * (unsigned)k.wts_ld + (unsigned)lane_ch(t)) * (unsigned)sizeof(T);
+            asm volatile("" : "+v"(off));
+            char* fb = (char*)((T*)k.wts + t.bb * k.wts_b) + n * k.wts_nb;
             __builtin_nontemporal_store(v, (u32x4_t*)(fb + off));
         }
     };
-    // softmax over the frames on the accumulators (xb: the features -> the packed weights), the fused sum
-    // stored now; the accumulators restart from zero
-    // xb: the frames' features (16-B loads, issued first so their latency overlaps the softmax), turned in place
-    // into the packed fusion weights, each frame's stored as soon as it is computed.  (Spreading these loads and stores over the MFMA stages measured slower: a
+    // xb: a ring of NH frames' features (16-B loads; the first NH issued first, so their latency overlaps the
+    // softmax, each later one as its slot's frame is consumed); each frame's weights are stored as computed.  (Spreading these loads and stores over the MFMA stages measured slower: a
     // wave's vector-memory operations complete in issue order, so an HBM load ahead of the next stage's LDS-DMA
     // pieces delays the barrier that waits for them.)
+    constexpr int NH = (NF + 1) / 2;     // feature registers: a ring of half the frames
     auto epilogue = [&](const Tile& t) {
-        u32x4_t xb[NF];
-#pragma unroll
-        for (int n = 0; n < NF; ++n) feat_load(t, n, xb[n]);
+        u32x4_t xb[NH];
+        StaticFor<0, NH>::run([&](auto n_) { feat_load(t, decltype(n_)::value, xb[decltype(n_)::value]); });
         const int ch = lane_ch(t);
         const float4 b0 = *(const float4*)(lbias + ch), b1 = *(const float4*)(lbias + ch + 4);
         const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
@@ -216,12 +253,13 @@ __global__ __launch_bounds__(512, 1) void conv_fuse_kernel(FuseK k, int tiles_x,
         if constexpr ((DBSR_FUSE_ABL & 1) != 0) {         // (timing only: every accumulator consumed, cheaply)
 #pragma unroll
             for (int e = 0; e < 8; ++e) fz[e] = bv[e];
+            StaticFor<0, NF>::run([&](auto n_) {
+                constexpr int n = decltype(n_)::value;
 #pragma unroll
-            for (int n = 0; n < NF; ++n) {
-#pragma unroll
-                for (int e = 0; e < 8; ++e) fz[e] += acc[n][e >> 2][e & 3];
+                for (int e = 0; e < 8; ++e) fz[e] += acc[n][e >> 2][e & 3] + H16<T>::lo(xb[n % NH][e >> 1]);
+                if constexpr (n + NH < NF) feat_load(t, n + NH, xb[n % NH]);
                 acc[n][0] = acc[n][1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-            }
+            });
         } else {
 #pragma unroll
             for (int e = 0; e < 8; ++e) m[e] = -INFINITY;
@@ -248,20 +286,24 @@ __global__ __launch_bounds__(512, 1) void conv_fuse_kernel(FuseK k, int tiles_x,
                 inv[e] = 1.0f / sum[e];
                 fz[e] = 0.f;
             }
-#pragma unroll
-            for (int n = 0; n < NF; ++n) {
+            // frame by frame: weights, their store, the weighted features; frame n's feature register then takes
+            // frame n + NH's load
+            StaticFor<0, NF>::run([&](auto n_) {
+                constexpr int n = decltype(n_)::value;
                 float w[8];
+                u32x4_t o;
 #pragma unroll
                 for (int e = 0; e < 8; ++e) w[e] = acc[n][e >> 2][e & 3] * inv[e];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    fz[2 * j] = fmaf(H16<T>::lo(xb[n][j]), w[2 * j], fz[2 * j]);
-                    fz[2 * j + 1] = fmaf(H16<T>::hi(xb[n][j]), w[2 * j + 1], fz[2 * j + 1]);
-                    xb[n][j] = H16<T>::pack(w[2 * j], w[2 * j + 1]);
+                    fz[2 * j] = fmaf(H16<T>::lo(xb[n % NH][j]), w[2 * j], fz[2 * j]);
+                    fz[2 * j + 1] = fmaf(H16<T>::hi(xb[n % NH][j]), w[2 * j + 1], fz[2 * j + 1]);
+                    o[j] = H16<T>::pack(w[2 * j], w[2 * j + 1]);
                 }
-                store_w(t, n, xb[n]);
+                if constexpr (n + NH < NF) feat_load(t, n + NH, xb[n % NH]);
+                store_w(t, n, o);
                 acc[n][0] = acc[n][1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-            }
+            });
         }
         u32x4_t o;
 #pragma unroll
@@ -269,37 +311,54 @@ __global__ __launch_bounds__(512, 1) void conv_fuse_kernel(FuseK k, int tiles_x,
         *(u32x4_t*)((T*)k.fused + t.bb * k.fus_b + lane_pix(t) * k.fus_ld + ch) = o;
     };
 
-    const int nst = k.nchunks * 3;
-    int s = 0;                          // global stage index (LDS buffer = s & 1)
+    int s3 = 0;                         // stage index mod 3 (weight ring buffer)
+    int gc = 0;                         // global chunk number (row ring slots)
     Tile cur = decode(0), prev = cur;
+    // prologue: stages 0 and 1 of the first super-tile
 #pragma unroll
-    for (int it = 0; it < C::PER; ++it) dma(it, cur, 0, 0, 0);
+    for (int it = 0; it < C::PER2; ++it) dma(it, cur, 0, 0, 0, 0);
+#pragma unroll
+    for (int it = 0; it < C::PER1; ++it) dma(it, cur, 0, 1, 0, 1);
+    int pending = C::PER1;              // this wave's pieces of the stage after the current one (in flight)
 
     for (int ti = 0; ti < my_tiles; ++ti) {
+        const bool has_next = ti + 1 < my_tiles;
+        const Tile nxt = has_next ? decode(ti + 1) : cur;
         int c = 0, ky = 0;
-        for (int st = 0; st < nst; ++st, ++s) {
-            dma_barrier();              // stage s landed (every wave's pieces); stage s-1 fully consumed
-            if (st == 0 && ti > 0) epilogue(prev);
-            const bool last = st == nst - 1;
-            const bool more = !(last && ti + 1 == my_tiles);
-            Tile nxt = cur;
-            int nc = ky == 2 ? c + 1 : c, nky = ky == 2 ? 0 : ky + 1;
-            if (last) {
-                nc = 0;
-                nky = 0;
-                if (more) nxt = decode(ti + 1);
+        for (int st = 0; st < 3 * k.nchunks; ++st) {
+            // stage (c, ky) landed: every wave waits for its own pieces of it (the next stage's may still be in
+            // flight), then the barrier makes every wave's visible
+            switch (pending) {
+                case C::PER1: DBSR_VM_WAIT(C::PER1); break;
+                case C::PER2: DBSR_VM_WAIT(C::PER2); break;
+                default: vm_drain(); break;
             }
-            const u32x4_t* lb = lds + (s & 1) * C::STAGE_U4;
-            const int nbuf = (s + 1) & 1;
+            __syncthreads();
+            if (st == 0 && ti > 0) epilogue(prev);
+            // the stage two ahead: (c, 2) from ky 0, else kernel row ky - 1 of the next chunk, which may be the next
+            // super-tile's first
+            const int ky2 = ky == 0 ? 2 : ky - 1;
+            int c2 = ky == 0 ? c : c + 1;
+            Tile t2 = cur;
+            bool issue = true;
+            if (c2 == k.nchunks) {
+                c2 = 0;
+                t2 = nxt;
+                issue = has_next;
+            }
+            const int gc2 = ky == 0 ? gc : gc + 1, wb2 = s3 == 0 ? 2 : s3 - 1;
+            const u32x4_t* lw = lds + s3 * C::W_U4;
+            // this wave's B row: kernel row ky + wr of the chunk
+            const u32x4_t* lr = lds + C::ROWS_OFF + ((4 * gc + ky + wr) % C::NROW) * C::ROW_U4;
             // the stage's 3 taps x N frames as one flat sequence of steps q = kx*N + n; each step's B-fragment is
-            // read PD steps ahead (a ring of PD registers) and the next tap's A-fragments one tap ahead, so the
-            // LDS latency hides behind the MFMAs instead of a wait before every MFMA pair
+            // read PD steps ahead (a ring of PD registers) and the next tap's A-fragments one tap ahead, so the LDS
+            // latency hides behind the MFMAs instead of a wait before every MFMA pair
             auto read_a = [&](int kx, int i) {
-                return __builtin_bit_cast(bf16x8_t, lb[a_base + (kx * (C::WM / 16) + i) * 64]);
+                return __builtin_bit_cast(bf16x8_t, lw[a_base + (kx * (C::WM / 16) + i) * 64]);
             };
             auto read_b = [&](int q) {
-                const int kx = q / NF, n = q % NF;
-                return __builtin_bit_cast(bf16x8_t, lb[(C::W_ITEMS + n * C::HP) * 64 + in_base[kx]]);
+                const int m = (q % NF) * C::HWD + q / NF;
+                return __builtin_bit_cast(bf16x8_t, lr[base8[m & 7] + 4 * m]);
             };
             constexpr int PD = 6, NQ = 3 * NF;
             bf16x8_t bq[PD], a[2][2];
@@ -314,11 +373,17 @@ __global__ __launch_bounds__(512, 1) void conv_fuse_kernel(FuseK k, int tiles_x,
                         a[(kx + 1) & 1][0] = read_a(kx + 1, 0);
                         a[(kx + 1) & 1][1] = read_a(kx + 1, 1);
                     }
-                    // the next stage's pieces, a third of them per tap between this stage's MFMAs
-                    if (more) {
+                    // the pieces of the stage two ahead, a third of them per tap between this stage's MFMAs
+                    if (issue) {
+                        if (ky2 == 0) {
 #pragma unroll
-                        for (int it = 0; it < C::PER; ++it)
-                            if ((it * 3) / C::PER == kx) dma(it, nxt, nc, nky, nbuf);
+                            for (int it = 0; it < C::PER2; ++it)
+                                if ((it * 3) / C::PER2 == kx) dma(it, t2, c2, ky2, gc2, wb2);
+                        } else {
+#pragma unroll
+                            for (int it = 0; it < C::PER1; ++it)
+                                if ((it * 3) / C::PER1 == kx) dma(it, t2, c2, ky2, gc2, wb2);
+                        }
                     }
                 }
                 const bf16x8_t b = bq[q % PD];
@@ -327,15 +392,21 @@ __global__ __launch_bounds__(512, 1) void conv_fuse_kernel(FuseK k, int tiles_x,
                 acc[n][1] = mfma16<T>(a[kx & 1][1], b, acc[n][1]);
                 __builtin_amdgcn_sched_barrier(0);      // keep the ring's order (the scheduler re-serialises it)
             });
-            c = nc;
-            ky = nky;
-            if (last) {
-                prev = cur;
-                cur = nxt;
+            pending = !issue ? 0 : ky2 == 0 ? C::PER2 : C::PER1;
+            s3 = s3 == 2 ? 0 : s3 + 1;
+            if (ky == 2) {
+                ky = 0;
+                ++c;
+                ++gc;
+            } else {
+                ++ky;
             }
         }
+        prev = cur;
+        cur = nxt;
     }
-    dma_barrier();                      // (the epilogue reads no LDS but the bias; keeps the DMA queue drained)
+    vm_drain();                         // (the epilogue reads no LDS but the bias; keeps the DMA queue drained)
+    __syncthreads();
     epilogue(prev);
 }
 
@@ -428,14 +499,29 @@ extern "C" int dbsr_conv_fuse_softmax(const dbsr_conv_desc* d, int B, int N, dbs
     k.ref = (const char*)ref.ptr + (base + ref.c0) * esz; k.ref_b = sb; k.ref_ld = ref.ld;
     DBSR_CHECK_ARG(affine_frames(oth, B, N - 1, N - 1, 1, 0, base, sb, sn), "conv_fuse_softmax: oth frame map not affine");
     k.oth = (const char*)oth.ptr + (base + oth.c0) * esz; k.oth_b = sb; k.oth_n = sn; k.oth_ld = oth.ld;
+    {
+        const long long span = ((N - 2) * sn + C + (long long)(hw - 1) * oth.ld) * esz;
+        DBSR_CHECK_ARG(sn >= 0 && span < (1LL << 31), "conv_fuse_softmax: a burst's other frames span >= 2 GiB");
+        k.oth_span = (unsigned)span;
+        k.oth_nb = (int)(sn * esz);
+    }
+    {
+        const long long span = ((long long)C + (long long)(hw - 1) * ref.ld) * esz;
+        DBSR_CHECK_ARG(span < (1LL << 31), "conv_fuse_softmax: ref frame >= 2 GiB");
+        k.ref_span = (unsigned)span;
+    }
     DBSR_CHECK_ARG(affine_frames(fused, B, 1, 1, 0, 0, base, sb, sn), "conv_fuse_softmax: fused frame map not affine");
     k.fused = (char*)fused.ptr + (base + fused.c0) * esz; k.fus_b = sb; k.fus_ld = fused.ld;
     if (weights.ptr) {
         DBSR_CHECK_ARG(affine_frames(weights, B, N, N, 1, 0, base, sb, sn),
                        "conv_fuse_softmax: weights frame map not affine");
         k.wts = (char*)weights.ptr + (base + weights.c0) * esz; k.wts_b = sb; k.wts_n = sn; k.wts_ld = weights.ld;
+        const long long span = ((N - 1) * sn + C + (long long)(hw - 1) * weights.ld) * esz;
+        DBSR_CHECK_ARG(sn >= 0 && span < (1LL << 31), "conv_fuse_softmax: a burst's fusion weights span >= 2 GiB");
+        k.wts_span = (unsigned)span;
+        k.wts_nb = (int)(sn * esz);
     } else {
-        k.wts = nullptr; k.wts_b = k.wts_n = 0; k.wts_ld = 0;
+        k.wts = nullptr; k.wts_b = k.wts_n = 0; k.wts_ld = 0; k.wts_span = 0; k.wts_nb = 0;
     }
     const int tiles_x = k.W / 16, tiles_y = k.H / 2, nct = C / FUSE_WM;
     const long long nt = (long long)B * tiles_x * tiles_y * nct;

@@ -10,9 +10,9 @@ export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_gpu_fuse.py -x -v --timeout 120 --timeout-method thread \
     > $out/pytest_fuse.log 2>&1 || { echo "fuse tests failed rc=$?"; grep -E "FAIL|Error|assert|Mismatch" $out/pytest_fuse.log | head -30; tail -5 $out/pytest_fuse.log; exit 1; }
 tail -1 $out/pytest_fuse.log
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread \
     > $out/pytest.log 2>&1 || { echo "pytest failed rc=$?"; grep -E "FAIL|Error|assert" $out/pytest.log | head -30; tail -5 $out/pytest.log; exit 1; }
-tail -1 $out/pytest.log
+tail -1 $out/pytest.log; grep "precision vs oracle" $out/pytest.log
 timeout -k 10 300 python bench.py --kernel-breakdown --no-cpu-baseline ${@:2} > $out/bench.json 2> $out/bench.err || { echo bench failed; tail -20 $out/bench.err; exit 1; }
 python -c "import json;d=json.load(open('$out/bench.json'));print('fp16', d['value'], d['ms_per_step'], {k: v['frac'] for k, v in d['roofline_families'].items()})"
 grep "^\[family\]" $out/bench.err | head -14

@@ -25,7 +25,7 @@ DMA_RE = re.compile(r'\b(buffer_load_\w+\b.*\blds\b|global_load_lds_\w+)')
 # issued after the barrier overwrite was read before it), so the drain rule becomes: a vmcnt wait between the
 # wave's last DMA and every barrier.  Its 9-wave blocks cannot own their SIMDs (3 waves on one SIMD); it is a
 # training-step kernel, issued on the trainer's one stream (no second lane runs beside the backward).
-RING_KERNELS = ('conv_wgrad_dma_kernel',)
+RING_KERNELS = ('conv_wgrad_dma_kernel', 'conv_fuse_kernel')
 
 
 def code_objects(so_path):
