@@ -38,7 +38,7 @@ using namespace dbsr;
 
 // Ablation switches for same-box A/B builds only (tools/build_variant.sh; the product build compiles none of
 // them): bit 1 replaces the epilogue's softmax by a plain sum of the accumulators, 2 skips the halo DMA, 4 the
-// weight DMA
+// weight DMA, 8 the feature loads, 16 the stage barriers
 #ifndef DBSR_FUSE_ABL
 #define DBSR_FUSE_ABL 0
 #endif
@@ -245,7 +245,12 @@ __global__ __launch_bounds__(512, 1) void conv_fuse_kernel(FuseK k, int tiles_x,
     constexpr int NH = (NF + 1) / 2;     // feature registers: a ring of half the frames
     auto epilogue = [&](const Tile& t) {
         u32x4_t xb[NH];
-        StaticFor<0, NH>::run([&](auto n_) { feat_load(t, decltype(n_)::value, xb[decltype(n_)::value]); });
+        StaticFor<0, NH>::run([&](auto n_) {
+            if constexpr ((DBSR_FUSE_ABL & 8) != 0)         // (timing only: no feature loads)
+                xb[decltype(n_)::value] = __builtin_bit_cast(u32x4_t, acc[decltype(n_)::value][0]);
+            else
+                feat_load(t, decltype(n_)::value, xb[decltype(n_)::value]);
+        });
         const int ch = lane_ch(t);
         const float4 b0 = *(const float4*)(lbias + ch), b1 = *(const float4*)(lbias + ch + 4);
         const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
@@ -257,7 +262,7 @@ __global__ __launch_bounds__(512, 1) void conv_fuse_kernel(FuseK k, int tiles_x,
                 constexpr int n = decltype(n_)::value;
 #pragma unroll
                 for (int e = 0; e < 8; ++e) fz[e] += acc[n][e >> 2][e & 3] + H16<T>::lo(xb[n % NH][e >> 1]);
-                if constexpr (n + NH < NF) feat_load(t, n + NH, xb[n % NH]);
+                if constexpr (n + NH < NF && (DBSR_FUSE_ABL & 8) == 0) feat_load(t, n + NH, xb[n % NH]);
                 acc[n][0] = acc[n][1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
             });
         } else {
@@ -333,7 +338,7 @@ __global__ __launch_bounds__(512, 1) void conv_fuse_kernel(FuseK k, int tiles_x,
                 case C::PER2: DBSR_VM_WAIT(C::PER2); break;
                 default: vm_drain(); break;
             }
-            __syncthreads();
+            if constexpr ((DBSR_FUSE_ABL & 16) == 0) __syncthreads();   // (timing only: no barrier)
             if (st == 0 && ti > 0) epilogue(prev);
             // the stage two ahead: (c, 2) from ky 0, else kernel row ky - 1 of the next chunk, which may be the next
             // super-tile's first
