@@ -1,5 +1,6 @@
 // Shared device helpers for the gfx950 DBSR kernels.
 #pragma once
+#include <type_traits>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "../../include/dbsr_hip.h"
@@ -11,6 +12,7 @@ typedef _Float16 f16_t;                                             // fp16 stor
 typedef __attribute__((ext_vector_type(8))) short bf16x8_t;        // MFMA 16-bit operand (8 elems, raw bits)
 typedef __attribute__((ext_vector_type(4))) float f32x4_t;          // 16x16 MFMA accumulator
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
+typedef __attribute__((ext_vector_type(2))) unsigned int u32x2_t;
 
 // The LDS-DMA-staged MFMA conv kernels (pipelined, weight-stationary, two-barrier tiled) claim the whole VGPR
 // file of their SIMDs (v255 marked live -> 256 VGPRs per wave; their 2 waves per SIMD then fill its 512), so no
@@ -137,6 +139,56 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uns
 __device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t r, int voff, int soff, u32x4_t* lds_piece) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_piece, 16, voff, soff, 0, 0);
 }
+
+// 3x3 Gaussian blur (upsampling.py:24-29, 59-65) as a separable pair -- the reference's kernel is the normalised
+// outer product of a 1-D Gaussian -- horizontal taps kh, vertical taps kv.  Every blur kernel of the library sums
+// in this order (blur_row, then blur_col), so their outputs are bitwise equal to one another.
+struct Blur3 {
+    float kh[3], kv[3];
+};
+// k9 (row-major 3x3) -> kh = its middle row, kv = its middle column / k[4]; false unless k9 = kv kh^T to 1e-6
+inline bool blur_separable(const float* k9, Blur3& b) {
+    if (!(k9[4] > 0.f)) return false;
+    float mx = 0.f;
+    for (int i = 0; i < 9; ++i) mx = k9[i] > mx ? k9[i] : (-k9[i] > mx ? -k9[i] : mx);
+    for (int j = 0; j < 3; ++j) b.kh[j] = k9[3 + j];
+    for (int i = 0; i < 3; ++i) b.kv[i] = k9[3 * i + 1] / k9[4];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            const float d = k9[3 * i + j] - b.kv[i] * b.kh[j];
+            if (d > 1e-6f * mx || -d > 1e-6f * mx) return false;
+        }
+    return true;
+}
+// horizontal pass over one row of 8 channels: x0, x1, x2 = columns -1, 0, +1 (16-bit, raw)
+template <typename T>
+__device__ __forceinline__ void blur_row(const Blur3& b, const u32x4_t& x0, const u32x4_t& x1, const u32x4_t& x2,
+                                         float (&h)[8]) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        h[2 * q] = fmaf(b.kh[2], H16<T>::lo(x2[q]), fmaf(b.kh[1], H16<T>::lo(x1[q]), b.kh[0] * H16<T>::lo(x0[q])));
+        h[2 * q + 1] = fmaf(b.kh[2], H16<T>::hi(x2[q]), fmaf(b.kh[1], H16<T>::hi(x1[q]), b.kh[0] * H16<T>::hi(x0[q])));
+    }
+}
+// vertical pass: rows -1, 0, +1 of horizontal sums
+__device__ __forceinline__ void blur_col(const Blur3& b, const float (&h0)[8], const float (&h1)[8], const float (&h2)[8],
+                                         float (&o)[8]) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[q] = fmaf(b.kv[2], h2[q], fmaf(b.kv[1], h1[q], b.kv[0] * h0[q]));
+}
+
+// compile-time loop: f(std::integral_constant<int, I>) for I in [I0, I1) (register arrays indexed by I stay
+// in registers whatever the unroller decides)
+template <int I0, int I1>
+struct StaticFor {
+    template <class F>
+    __device__ __forceinline__ static void run(F&& f) {
+        if constexpr (I0 < I1) {
+            f(std::integral_constant<int, I0>{});
+            StaticFor<I0 + 1, I1>::run(f);
+        }
+    }
+};
 
 }  // namespace dbsr
 

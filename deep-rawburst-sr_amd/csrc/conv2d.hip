@@ -1891,24 +1891,21 @@ __global__ __launch_bounds__(512) void upsample_shuffle_kernel(ConvK k) {
     if (sub < s2) load_a(sub, a_cur);
     for (; sub < s2; sub += 8) {
         if (sub + 8 < s2) load_a(sub + 8, a_nxt);
+        // the bias is the accumulators' initial value (bias + sum_k, the order upsample_blur_kernel sums in)
+        f32x4_t bq[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
+        if (k.bias) {
+            bq[0] = *(const f32x4_t*)(k.bias + sub * 32 + 8 * g);
+            bq[1] = *(const f32x4_t*)(k.bias + sub * 32 + 8 * g + 4);
+        }
         f32x4_t acc[2][PG];
 #pragma unroll
         for (int h = 0; h < 2; ++h)
 #pragma unroll
             for (int j = 0; j < PG; ++j) {
-                acc[h][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+                acc[h][j] = bq[h];
 #pragma unroll
                 for (int ks = 0; ks < KS; ++ks) acc[h][j] = mma(a_cur[h][ks], b[j][ks], acc[h][j]);
             }
-        const float* bp = k.bias + sub * 32 + 8 * g;
-        float bv[8];
-        if (k.bias) {
-            const float4 b0 = *(const float4*)bp, b1 = *(const float4*)(bp + 4);
-            bv[0] = b0.x; bv[1] = b0.y; bv[2] = b0.z; bv[3] = b0.w; bv[4] = b1.x; bv[5] = b1.y; bv[6] = b1.z; bv[7] = b1.w;
-        } else {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) bv[e] = 0.f;
-        }
         const int sy = sub / s, sx = sub - sy * s;
 #pragma unroll
         for (int j = 0; j < PG; ++j) {
@@ -1916,10 +1913,8 @@ __global__ __launch_bounds__(512) void upsample_shuffle_kernel(ConvK k) {
             u32x4_t o;
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
-                o[e] = H16<T>::pack(apply_act(acc[0][j][2 * e] + bv[2 * e], k.act),
-                                   apply_act(acc[0][j][2 * e + 1] + bv[2 * e + 1], k.act));
-                o[2 + e] = H16<T>::pack(apply_act(acc[1][j][2 * e] + bv[4 + 2 * e], k.act),
-                                       apply_act(acc[1][j][2 * e + 1] + bv[4 + 2 * e + 1], k.act));
+                o[e] = H16<T>::pack(apply_act(acc[0][j][2 * e], k.act), apply_act(acc[0][j][2 * e + 1], k.act));
+                o[2 + e] = H16<T>::pack(apply_act(acc[1][j][2 * e], k.act), apply_act(acc[1][j][2 * e + 1], k.act));
             }
             const long long Y = (long long)py[j] * s + sy, X = (long long)px[j] * s + sx;
             *(u32x4_t*)((T*)k.y + map_frame(k.ym, pf[j]) * k.y_is + (Y * (k.out_w * s) + X) * k.y_ld + k.y_c0 +
@@ -1955,6 +1950,257 @@ int launch_upsample(const ConvK& k, hipStream_t s) {
 #undef DBSR_UP
     DBSR_LAUNCH_CHECK();
     return 0;
+}
+
+// ------------------------------------------------------------------------------------------------
+// PixelShuffle upsampler + Gaussian blur in one pass (upsampling.py:51-66, decoders.py:43): the
+// decoder's 1x1 conv Cin -> 64 x 32 (+ bias, act), PixelShuffle(8) and the 3x3 depthwise blur with zero
+// padding, without the pre-blur tensor's HBM round trip (75.5 MB written and read back at the bench shape).
+//
+// Persistent blocks of 8 waves (2 per SIMD).  Wave w keeps in registers the packed weight rows of output
+// channels 4w..4w+3 for all 64 sub-pixels: 16 row blocks x KS k-steps (128 VGPRs at Cin 64).  Work unit =
+// a 4x4 low-res tile = 32x32 output pixels.  Conv phase: the tile's 16 pixels and its ring of 20 (three
+// 16-pixel MFMA column groups) run through the row blocks; lane (g, col) of row block rb gets channels
+// 4w..4w+3 of sub-pixel (rb / 2, 4(rb & 1) + g) of pixel col, which -- + bias, act, rounded to T exactly as
+// upsample_shuffle_kernel stores it -- goes to an LDS image of the tile's 32x32 output pixels plus a 1-pixel
+// halo (of a ring pixel only the sub-pixels inside that halo are computed and kept; pixels outside the frame
+// are zeros, the blur's padding).  Blur phase: thread (strip, column, 8-channel group) slides a 3-row window
+// of horizontal sums down 8 output rows (the separable Gaussian: blur_row / blur_col, as blur3_h16_kernel
+// sums), so the output is bitwise that of dbsr_conv2d followed by dbsr_gauss_blur3.  The image is double-buffered: one barrier per tile.
+// Image pixel (Ys, Xs) = 64 B = 8 positions of 4 channels; channel quad q sits at position q ^ key, key =
+// (Lx & 3) | (Ly & 1) << 2 of the pixel's low-res coordinates in the ringed tile, (Ly, Lx) = ((Ys + 7) / 8,
+// (Xs + 7) / 8): the 16 lanes of a conv-phase ds_write_b64 (one sub-pixel of 16 low-res pixels, which
+// without the key share one address mod 128 B) then hit 8 distinct positions (2-way, the minimum).
+// ------------------------------------------------------------------------------------------------
+#ifndef DBSR_UB_ABL
+#define DBSR_UB_ABL 0        // timing-only ablations: 1 no conv phase, 2 no blur phase, 4 no blur stores
+#endif
+// ReLU of two packed 16-bit floats (bf16 or fp16) on their bit patterns: a signed 16-bit max with 0 zeroes every
+// negative value and -0, so relu16x2(pack(x)) == pack(max(x, 0)) bitwise
+__device__ __forceinline__ unsigned relu16x2(unsigned v) {
+    typedef short s16x2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(unsigned, __builtin_elementwise_max(__builtin_bit_cast(s16x2, v), s16x2{0, 0}));
+}
+namespace ub {
+constexpr int LT = 4, S = 8, HS = LT * S + 2, NPX = HS * HS;      // image: HS x HS pixels
+constexpr int IMG_U2 = NPX * 8;                                   // ... in 8-B units
+constexpr int ROWS = 2048;                                        // conv rows: 64 sub-pixels x 32 channels
+__host__ __device__ constexpr int key(int Ly, int Lx) { return (Lx & 3) | ((Ly & 1) << 2); }
+// ringed-tile coordinates (Ly, Lx) in [0, 6)^2 of column c of group G (0: the 16 interior pixels, 1 and 2:
+// the 20 ring pixels: top row, bottom row, left column, right column); false past the ring
+__device__ __forceinline__ bool ring_px(int G, int c, int& Ly, int& Lx) {
+    if (G == 0) { Ly = 1 + (c >> 2); Lx = 1 + (c & 3); return true; }
+    const int r = (G - 1) * 16 + c;
+    if (r < 6) { Ly = 0; Lx = r; }
+    else if (r < 12) { Ly = 5; Lx = r - 6; }
+    else if (r < 16) { Ly = r - 11; Lx = 0; }
+    else if (r < 20) { Ly = r - 15; Lx = 5; }
+    else { Ly = 0; Lx = 0; return false; }
+    return true;
+}
+// row blocks whose sub-pixels reach the halo of group G's pixels: group 1 (top: sub-row 7 = rb 14, 15;
+// bottom: sub-row 0 = rb 0, 1; left: sub-column 7 = odd rb) and group 2 (right: sub-column 0 = even rb)
+constexpr bool rb_used(int G, int rb) {
+    return G == 0 || (G == 1 && (rb >= 14 || rb <= 1 || (rb & 1))) || (G == 2 && !(rb & 1));
+}
+}  // namespace ub
+
+template <typename T, int KS, int ACT>
+__global__ __launch_bounds__(512, 1) void upsample_blur_kernel(ConvK k, Blur3 kb, int tiles_x, int tiles_y,
+                                                               int ntiles) {
+    using namespace ub;
+    auto act = [](float v) { return apply_act(v, ACT); };        // (compile-time: a runtime act branched per value)
+    constexpr int UB_BATCH = KS == 2 ? 2 : 4;                     // row blocks per MFMA batch (registers at KS 2)
+    __shared__ __attribute__((aligned(16))) u32x2_t img[2 * IMG_U2 + 64];   // + the conv phase's dummy slots
+    __shared__ __attribute__((aligned(16))) float lbias[ROWS];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int g = lane >> 4, col = lane & 15;
+
+    // the wave's weight rows: row m of row block rb = sub-pixel 4 rb + m / 4, channel 4 wave + m % 4, packed as
+    // row sub * 32 + channel (dbsr_conv_pack_weights with shuffle)
+    Frag<T> wr[16][KS];
+#pragma unroll
+    for (int rb = 0; rb < 16; ++rb)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+            wr[rb][ks].load((const T*)k.w + (long long)((4 * rb + (col >> 2)) * 32 + 4 * wave + (col & 3)) * k.Kp +
+                            ks * 32 + g * 8);
+    for (int i = threadIdx.x; i < ROWS; i += 512) lbias[i] = k.bias ? k.bias[i] : 0.f;
+
+    const int Wh = k.in_w * S;                                    // output row length
+    auto decode = [&](int t, int& f, int& ty, int& tx) {
+        tx = t % tiles_x; t /= tiles_x;
+        ty = t % tiles_y; f = t / tiles_y;
+    };
+    // B-fragments of the three column groups of tile t (zeros outside the frame / past the ring)
+    auto load_b = [&](int t, Frag<T> (&b)[3][KS]) {
+        int f, ty, tx;
+        decode(t, f, ty, tx);
+        const T* xf = (const T*)k.x + map_frame(k.xm, f) * k.x_is;
+#pragma unroll
+        for (int G = 0; G < 3; ++G) {
+            int Ly, Lx;
+            const bool in_ring = ring_px(G, col, Ly, Lx);
+            const int ly = ty * LT + Ly - 1, lx = tx * LT + Lx - 1;
+            const bool ok = in_ring && (unsigned)ly < (unsigned)k.in_h && (unsigned)lx < (unsigned)k.in_w;
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                if (ok) b[G][ks].load(xf + (long long)(ly * k.in_w + lx) * k.x_ld + ks * 32 + g * 8);
+                else b[G][ks].zero();
+            }
+        }
+    };
+
+    Frag<T> bcur[3][KS];
+    int t = blockIdx.x;
+    if (t < ntiles) load_b(t, bcur);
+    PIPE_STAMP(0);
+    __syncthreads();                                              // lbias
+    PIPE_STAMP(1);
+    for (int it = 0; t < ntiles; ++it, t += gridDim.x) {
+        int f, ty, tx;
+        decode(t, f, ty, tx);
+        u32x2_t* im = img + (it & 1) * IMG_U2;
+        // lane-derived values recomputed per tile from an opaque copy of the thread index: hoisted out of the loop,
+        // the conv phase's per-row-block LDS addresses and masks took ~40 registers and spilled
+        int tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        const int lane = tid & 63, g = lane >> 4, col = lane & 15;
+        PIPE_STAMP(2 + 4 * it);
+        // ---- conv phase ----
+        // branch-free: a lane whose sub-pixel falls outside the image writes its own dummy slot, pixels outside
+        // the frame write zeros; row blocks in batches (MFMAs of a batch, then its epilogue) so the
+        // compiler overlaps one batch's epilogue with the next batch's MFMAs
+        StaticFor<0, (DBSR_UB_ABL & 1) ? 0 : 3>::run([&](auto G_) {
+            constexpr int G = decltype(G_)::value;
+            int Ly, Lx;
+            const bool in_ring = ring_px(G, col, Ly, Lx);
+            const int ly = ty * LT + Ly - 1, lx = tx * LT + Lx - 1;
+            const bool inside = G == 0 || (in_ring && (unsigned)ly < (unsigned)k.in_h && (unsigned)lx < (unsigned)k.in_w);
+            const int pos = wave ^ key(Ly, Lx);                 // channel quad `wave`'s position
+            // byte address of this lane's quad in the image for row block 0 (row block rb adds a constant)
+            const int lb = (((8 * Ly - 7) * HS + 8 * Lx - 7 + g) * 8 + pos) * 8;
+            char* ib = (char*)(img + (it & 1) * IMG_U2) + lb;
+            StaticFor<0, 16 / UB_BATCH>::run([&](auto bt_) {
+                constexpr int bt = decltype(bt_)::value;
+                f32x4_t acc[UB_BATCH];
+                StaticFor<0, UB_BATCH>::run([&](auto j_) {
+                    constexpr int j = decltype(j_)::value, rb = UB_BATCH * bt + j;
+                    if constexpr (rb_used(G, rb)) {
+                        // the bias is the accumulator's initial value (as upsample_shuffle_kernel sums)
+                        acc[j] = *(const f32x4_t*)(lbias + (4 * rb + g) * 32 + 4 * wave);
+#pragma unroll
+                        for (int ks = 0; ks < KS; ++ks) acc[j] = mma(wr[rb][ks], bcur[G][ks], acc[j]);
+                    }
+                });
+                StaticFor<0, UB_BATCH>::run([&](auto j_) {
+                    constexpr int j = decltype(j_)::value, rb = UB_BATCH * bt + j;
+                    if constexpr (!rb_used(G, rb)) return;
+                    constexpr int sy = rb >> 1, sx0 = 4 * (rb & 1);
+                    constexpr int off = (sy * HS + sx0) * 64;        // bytes past ib
+                    u32x2_t o;
+                    if constexpr (ACT == DBSR_ACT_RELU) {
+                        // ReLU on the rounded values' sign bits (v_pk_max_i16 with 0): bitwise the rounding of the
+                        // fp32 ReLU, -0 included
+                        o[0] = relu16x2(H16<T>::pack(acc[j][0], acc[j][1]));
+                        o[1] = relu16x2(H16<T>::pack(acc[j][2], acc[j][3]));
+                    } else {
+                        o[0] = H16<T>::pack(act(acc[j][0]), act(acc[j][1]));
+                        o[1] = H16<T>::pack(act(acc[j][2]), act(acc[j][3]));
+                    }
+                    if constexpr (G == 0) {
+                        *(u32x2_t*)(ib + off) = o;
+                    } else {
+                        const int Ys = 8 * Ly + sy - 7, Xs = 8 * Lx + sx0 + g - 7;
+                        const bool keep = in_ring && (unsigned)Ys < (unsigned)HS && (unsigned)Xs < (unsigned)HS;
+                        if (!inside) o = u32x2_t{0u, 0u};
+                        *(u32x2_t*)(keep ? ib + off : (char*)(img + 2 * IMG_U2 + lane)) = o;
+                    }
+                });
+            });
+        });
+        PIPE_STAMP(3 + 4 * it);
+        // the next tile's input pixels, in flight over the blur phase (issued before its stores)
+        if (t + (int)gridDim.x < ntiles) load_b(t + gridDim.x, bcur);
+        __syncthreads();
+        PIPE_STAMP(4 + 4 * it);
+        // ---- blur phase: thread = (strip of 8 output rows, output column, 8-channel group) ----
+        if constexpr ((DBSR_UB_ABL & 2) != 0) continue;
+        const int cg = tid & 3, ox = (tid >> 2) & 31, st = tid >> 7;
+        // raw 16-B read of the thread's 8 channels of image pixel (Ys, Xs) and its key's half swap (applied when the
+        // row enters the window, an iteration after its reads were issued)
+        auto raw = [&](int Ys, int Xs) {
+            const int ky = key((Ys + 7) >> 3, (Xs + 7) >> 3);
+            return *(const u32x4_t*)(im + (Ys * HS + Xs) * 8 + 2 * (cg ^ (ky >> 1)));
+        };
+        auto fix = [&](int Ys, int Xs, const u32x4_t& v) {
+            return (key((Ys + 7) >> 3, (Xs + 7) >> 3) & 1) ? u32x4_t{v[2], v[3], v[0], v[1]} : v;
+        };
+        T* yb = (T*)k.y + map_frame(k.ym, f) * k.y_is + k.y_c0 + 8 * cg +
+                ((long long)(ty * LT * S + 8 * st) * Wh + tx * LT * S + ox) * k.y_ld;
+        // horizontal sums of window rows r, r + 1, r + 2 in h0, h1, h2 (blur_row / blur_col: the separable Gaussian in
+        // blur3_h16_kernel's order); row r + 3's reads (wn) are issued an iteration ahead.  Unrolled with a scheduling
+        // fence per row (without it the compiler hoisted every LDS read and spilled)
+        const int y0 = 8 * st;
+        float h0[8], h1[8], h2[8];
+        {
+            u32x4_t a[3], b[3], c[3];
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                a[j] = raw(y0, ox + j);
+                b[j] = raw(y0 + 1, ox + j);
+                c[j] = raw(y0 + 2, ox + j);
+            }
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                a[j] = fix(y0, ox + j, a[j]);
+                b[j] = fix(y0 + 1, ox + j, b[j]);
+                c[j] = fix(y0 + 2, ox + j, c[j]);
+            }
+            blur_row<T>(kb, a[0], a[1], a[2], h0);
+            blur_row<T>(kb, b[0], b[1], b[2], h1);
+            blur_row<T>(kb, c[0], c[1], c[2], h2);
+        }
+        u32x4_t wn[3];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            __builtin_amdgcn_sched_barrier(0);              // (keeps each row's LDS reads in its own iteration)
+            const int yn = min(y0 + r + 3, HS - 1);       // (the last iteration's read is unused)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) wn[j] = raw(yn, ox + j);
+            float acc[8];
+            blur_col(kb, h0, h1, h2, acc);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                h0[q] = h1[q];
+                h1[q] = h2[q];
+            }
+#pragma unroll
+            for (int j = 0; j < 3; ++j) wn[j] = fix(yn, ox + j, wn[j]);
+            blur_row<T>(kb, wn[0], wn[1], wn[2], h2);
+            if constexpr ((DBSR_UB_ABL & 4) != 0) {
+                if (acc[0] == 123.f && acc[7] == 7.f) store8(yb, acc);
+            } else {
+                store8(yb + (long long)r * Wh * k.y_ld, acc);
+            }
+        }
+        PIPE_STAMP(5 + 4 * it);
+    }
+}
+
+// the fused upsampler + blur applies: 16-bit 1x1 conv Cin (<= 64, padded to 32 or 64) -> 64 sub-pixels x 32
+// channels, PixelShuffle(8), low-res frame a multiple of 4 x 4, aligned NHWC output
+bool use_upsample_blur(const dbsr_conv_desc* d) {
+    if (!d || !is16(d->x.dtype) || d->y.dtype != d->x.dtype || d->precise || d->out_mode != DBSR_OUT_SHUFFLE) return false;
+    if (d->shuffle != 8 || d->cout != 2048 || d->kh != 1 || d->kw != 1 || d->stride != 1 || d->pad != 0 ||
+        d->dil != 1 || d->res.ptr || d->gate.ptr)
+        return false;
+    const int cp = cin_pad(d->cin);
+    if (cp != 32 && cp != 64) return false;
+    if (d->in_h % ub::LT || d->in_w % ub::LT || d->in_h != d->out_h || d->in_w != d->out_w) return false;
+    if (d->x.ld % 8 || d->x.c0 % 8 || d->x.c0 + cp > d->x.ld) return false;
+    if (d->y.ld % 8 || d->y.c0 % 8 || d->y.c0 + 32 > d->y.ld) return false;
+    return (long long)d->n_frames * d->in_h * d->in_w * 64 < (1LL << 31);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2353,6 +2599,41 @@ extern "C" int dbsr_conv2d(const dbsr_conv_desc* d, void* stream) {
     if (use_pointwise(sel)) return d->x.dtype == DBSR_F16 ? launch_pointwise<f16_t>(k, s) : launch_pointwise<bf16_t>(k, s);
     if (d->x.dtype == DBSR_F16) return dispatch_conv<f16_t>(k, d, sel, s);
     return d->x.dtype == DBSR_BF16 ? dispatch_conv<bf16_t>(k, d, sel, s) : dispatch_conv<float>(k, d, sel, s);
+}
+
+extern "C" int dbsr_conv_shuffle_blur_ok(const dbsr_conv_desc* d) { return use_upsample_blur(d) ? 1 : 0; }
+
+extern "C" int dbsr_conv_shuffle_blur(const dbsr_conv_desc* d, const float* k9, void* stream) {
+    DBSR_CHECK_ARG(d && k9 && d->x.ptr && d->w && d->y.ptr, "conv_shuffle_blur: null pointer");
+    DBSR_CHECK_ARG(d->x.map.fpg > 0 && d->y.map.fpg > 0, "conv_shuffle_blur: frame map fpg must be > 0");
+    DBSR_CHECK_ARG(d->n_frames > 0, "conv_shuffle_blur: bad sizes");
+    DBSR_CHECK_ARG(use_upsample_blur(d), "conv_shuffle_blur: needs a 16-bit 1x1 conv cin <= 64 -> 2048 with "
+                   "PixelShuffle(8) output (32 channels), a low-res frame of multiples of 4, aligned NHWC slices");
+    const ConvK k = make_convk(d);
+    Blur3 kk;
+    DBSR_CHECK_ARG(blur_separable(k9, kk), "conv_shuffle_blur: the blur kernel must be separable (a Gaussian)");
+    const int tiles_x = d->in_w / ub::LT, tiles_y = d->in_h / ub::LT;
+    const int ntiles = d->n_frames * tiles_x * tiles_y;
+    int grid = d->max_blocks > 0 ? std::min(d->max_blocks, num_cus()) : num_cus();
+    grid = std::min(grid, ntiles);
+    hipStream_t s = (hipStream_t)stream;
+#define DBSR_UB(TT, KS, ACT) \
+    hipLaunchKernelGGL((upsample_blur_kernel<TT, KS, ACT>), dim3(grid), dim3(512), 0, s, k, kk, tiles_x, tiles_y, ntiles)
+#define DBSR_UB_ACT(TT, KS)                                   \
+    switch (d->act) {                                         \
+        case DBSR_ACT_RELU: DBSR_UB(TT, KS, DBSR_ACT_RELU); break;   \
+        case DBSR_ACT_LRELU: DBSR_UB(TT, KS, DBSR_ACT_LRELU); break; \
+        default: DBSR_UB(TT, KS, DBSR_ACT_NONE); break;             \
+    }
+    if (k.Kp == 64) {
+        if (d->x.dtype == DBSR_F16) { DBSR_UB_ACT(f16_t, 2) } else { DBSR_UB_ACT(bf16_t, 2) }
+    } else {
+        if (d->x.dtype == DBSR_F16) { DBSR_UB_ACT(f16_t, 1) } else { DBSR_UB_ACT(bf16_t, 1) }
+    }
+#undef DBSR_UB_ACT
+#undef DBSR_UB
+    DBSR_LAUNCH_CHECK();
+    return 0;
 }
 
 extern "C" int dbsr_conv2d_head(const dbsr_conv_desc* d, const float* head_w, const float* head_b, int head_cout,

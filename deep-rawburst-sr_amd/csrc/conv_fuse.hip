@@ -58,19 +58,6 @@ __device__ __forceinline__ f32x4_t mfma16(const bf16x8_t& a, const bf16x8_t& b, 
                                                       0, 0, 0);
 }
 
-// compile-time loop: f(std::integral_constant<int, I>) for I in [I0, I1) (register arrays indexed by I stay
-// in registers whatever the unroller decides)
-template <int I0, int I1>
-struct StaticFor {
-    template <class F>
-    __device__ __forceinline__ static void run(F&& f) {
-        if constexpr (I0 < I1) {
-            f(std::integral_constant<int, I0>{});
-            StaticFor<I0 + 1, I1>::run(f);
-        }
-    }
-};
-
 // One 1-KiB LDS-DMA piece issued from inline asm (as conv_wgrad_dma_kernel does): the compiler's wait insertion
 // does not see it, so it neither drains every outstanding piece before the fragment reads (it cannot tell the
 // ring stage being read from the stages being filled) nor at every __syncthreads; the kernel counts its own

@@ -609,9 +609,10 @@ __global__ __launch_bounds__(256) void blur3_kernel(int n, int h, int w, int gro
 }
 
 // 16-bit variant: every row load of the strip (ROWS + 2 rows x 3 columns, raw 16-B, 120 VGPRs at 8 rows)
-// is issued before the first FMA, so a thread waits one memory latency instead of one per row.
+// is issued before the first FMA, so a thread waits one memory latency instead of one per row.  The Gaussian
+// (separable: blur_separable) runs as blur_row + blur_col, the sums dbsr_conv_shuffle_blur uses (bitwise equal).
 template <typename T, int ROWS>
-__global__ __launch_bounds__(256) void blur3_h16_kernel(int n, int h, int w, int groups, dbsr_tensor in, K9 kk,
+__global__ __launch_bounds__(256) void blur3_h16_kernel(int n, int h, int w, int groups, dbsr_tensor in, Blur3 kb,
                                                         dbsr_tensor out) {
     const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     const int strips = (h + ROWS - 1) / ROWS;
@@ -635,21 +636,15 @@ __global__ __launch_bounds__(256) void blur3_h16_kernel(int n, int h, int w, int
             if ((unsigned)yy < (unsigned)h && (unsigned)xx < (unsigned)w)
                 raw[i][j] = *(const u32x4_t*)(base + ((long long)yy * w + xx) * in.ld);
         }
+    float hr[3][8];
+    blur_row<T>(kb, raw[0][0], raw[0][1], raw[0][2], hr[0]);
+    blur_row<T>(kb, raw[1][0], raw[1][1], raw[1][2], hr[1]);
 #pragma unroll
     for (int t = 0; t < ROWS; ++t) {
         const int y = y0 + t;
-        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-            for (int j = 0; j < 3; ++j) {
-                const float kv = kk.k[i * 3 + j];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    acc[2 * q] = fmaf(kv, H16<T>::lo(raw[t + i][j][q]), acc[2 * q]);
-                    acc[2 * q + 1] = fmaf(kv, H16<T>::hi(raw[t + i][j][q]), acc[2 * q + 1]);
-                }
-            }
+        blur_row<T>(kb, raw[t + 2][0], raw[t + 2][1], raw[t + 2][2], hr[(t + 2) % 3]);
+        float acc[8];
+        blur_col(kb, hr[t % 3], hr[(t + 1) % 3], hr[(t + 2) % 3], acc);
         if (y < h) store8(obase + ((long long)y * w + x) * out.ld, acc);
     }
 }
@@ -853,13 +848,21 @@ extern "C" int dbsr_gauss_blur3(int n, int h, int w, int c, dbsr_tensor in, cons
     DBSR_CHECK_ARG(c % 8 == 0 && vec_ok(in, 8) && vec_ok(out, 8), "blur: layout");
     K9 kk;
     for (int i = 0; i < 9; ++i) kk.k[i] = k_host[i];
+    Blur3 kb;
+    const bool sep = blur_separable(k_host, kb);
     const long long total = (long long)n * ((h + BLUR_ROWS - 1) / BLUR_ROWS) * w * (c / 8);
     return by_dtype(in.dtype, [&](auto* tag) {
         using T = std::remove_pointer_t<decltype(tag)>;
-        // 16-bit: load-first strips of 8 rows (dec.blur 38.0 -> 31.4 us; strips of 4 rows: 32.5 us)
+        // 16-bit, separable: load-first strips of 8 rows (dec.blur 38.0 -> 31.4 us; strips of 4 rows: 32.5 us)
         if constexpr (sizeof(T) == 2) {
+            if (!sep) {
+                hipLaunchKernelGGL(blur3_kernel<T>, dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, n,
+                                   h, w, c / 8, in, kk, out);
+                DBSR_LAUNCH_CHECK();
+                return 0;
+            }
             hipLaunchKernelGGL((blur3_h16_kernel<T, BLUR_ROWS>), dim3(nblocks(total, 256)), dim3(256), 0,
-                               (hipStream_t)stream, n, h, w, c / 8, in, kk, out);
+                               (hipStream_t)stream, n, h, w, c / 8, in, kb, out);
         } else
             hipLaunchKernelGGL(blur3_kernel<T>, dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, n, h,
                                w, c / 8, in, kk, out);

@@ -283,6 +283,22 @@ class Plan:
         self.kernel[len(self.ops) - 1] = 'conv_fuse'
         return len(self.ops) - 1
 
+    def conv_shuffle_blur(self, name, pc, n_frames, x, in_hw, y, act, k9):
+        """The PixelShuffle upsampler's conv + shuffle + 3x3 Gaussian blur in one launch
+        (dbsr_conv_shuffle_blur: the pre-blur tensor never reaches memory; upsampling.py:51-66).  Returns the
+        desc, or None when the library does not serve the shape (the caller then emits the conv and the blur)."""
+        d = self._desc(name, pc, n_frames, x, 0, in_hw, y, 0, act, IDENTITY, IDENTITY, None, 0, IDENTITY,
+                       L.ACT_NONE, L.OUT_SHUFFLE, pc.shuffle, None, None, False, None, 0, IDENTITY)
+        if not L.lib().dbsr_conv_shuffle_blur_ok(ctypes.byref(d)):
+            return None
+        kbuf = (ctypes.c_float * 9)(*k9)
+        self.keep.append(kbuf)
+        self.convs.append((d, self.lane))
+        flop = 2.0 * n_frames * d.out_h * d.out_w * pc.cout * d.cin
+        self.add(name, L.lib().dbsr_conv_shuffle_blur, ctypes.byref(d), kbuf, work=('flop', flop))
+        self.kernel[len(self.ops) - 1] = 'conv1x1_shuffle_blur'
+        return d
+
     def _desc(self, name, pc, n_frames, x, xc0, in_hw, y, yc0, act, xmap, ymap, res, rc0, rmap, post_act, out_mode,
               shuffle, y_desc, cin, precise, gate, gc0, gmap):
         oh, ow = pc.out_hw(*in_hw)
@@ -613,6 +629,8 @@ class DBSREngine:
     LANE0_CU_SHARE = 0.5      # CU share of lane 0's persistent convs while the PWC lane runs (tools/capbench.sh)
     # bf16: fuse the RGB predictor into the last decoder ResBlock conv (False: separate fp32 kernel)
     FUSED_HEAD = True
+    # PixelShuffle upsampler conv + shuffle + blur in one kernel (dbsr_conv_shuffle_blur)
+    FUSED_UPSAMPLE_BLUR = True
     # weight-predictor input conv split into a per-frame [proj, offfeat] conv + a per-burst base conv
     LINEAR_SPLIT = True
     # weight-predictor output conv + softmax + fusion in one kernel (dbsr_conv_fuse_softmax: the fp32 logits never
@@ -948,13 +966,20 @@ class DBSREngine:
         pc = self.dec_up.cout // (S * S)
         sh = [NHWC(B, H * S, W * S, pc, dt, dev) for _ in range(3)]
         a = 0
-        plan.conv('dec.upsample', self.dec_up, B, g[i], 0, hw, sh[0], 0, L.ACT_RELU, out_mode=L.OUT_SHUFFLE,
-                  shuffle=S)
-        if self.blur is not None:
-            kbuf = (ctypes.c_float * 9)(*self.blur)
-            plan.keep.append(kbuf)
-            plan.add('dec.blur', lib.dbsr_gauss_blur3, B, H * S, W * S, pc, sh[0].d(0), kbuf, sh[1].d(0))
+        # conv + PixelShuffle + blur in one kernel where the library serves the shape (the pre-blur tensor, 75.5 MB
+        # at the bench shape, then never round-trips through HBM; bitwise equal to the two launches)
+        if self.blur is not None and DBSREngine.FUSED_UPSAMPLE_BLUR and \
+                plan.conv_shuffle_blur('dec.upsample+blur', self.dec_up, B, g[i], hw, sh[1], L.ACT_RELU,
+                                       self.blur) is not None:
             a = 1
+        else:
+            plan.conv('dec.upsample', self.dec_up, B, g[i], 0, hw, sh[0], 0, L.ACT_RELU, out_mode=L.OUT_SHUFFLE,
+                      shuffle=S)
+            if self.blur is not None:
+                kbuf = (ctypes.c_float * 9)(*self.blur)
+                plan.keep.append(kbuf)
+                plan.add('dec.blur', lib.dbsr_gauss_blur3, B, H * S, W * S, pc, sh[0].d(0), kbuf, sh[1].d(0))
+                a = 1
         if pred_out is None:
             pred_out = bufs['pred'] = torch.zeros(B, 3, H * S, W * S, dtype=torch.float32, device=dev)
         pdesc = L.tensor_desc(pred_out, 1, 0, img_stride=3 * H * S * W * S, dtype=torch.float32)

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define DBSR_ABI_VERSION 15
+#define DBSR_ABI_VERSION 16
 
 enum { DBSR_F32 = 0, DBSR_BF16 = 1, DBSR_F16 = 2 };
 enum { DBSR_ACT_NONE = 0, DBSR_ACT_RELU = 1, DBSR_ACT_LRELU = 2 };      /* LeakyReLU slope 0.1 */
@@ -139,6 +139,16 @@ int dbsr_conv_lane_reach(const dbsr_conv_desc* d, int which);
  * head_b: fp32 [head_cout] or NULL, head_cout 1..4.  Requires dbsr_conv_head_ok(d). */
 int dbsr_conv2d_head(const dbsr_conv_desc* d, const float* head_w, const float* head_b, int head_cout,
                      dbsr_tensor head_out, void* stream);
+/* PixelShuffle upsampler + Gaussian blur in one launch (ABI 16; upsampling.py:51-66, replaces the pair
+ * dbsr_conv2d(d) -> dbsr_gauss_blur3 of decoders.py:57's upsample_layer): y = blur3(PixelShuffle(act(conv1x1(x)
+ * + bias))), k9 = the 3x3 blur kernel (host, row-major; separable, as the reference's Gaussian is, else
+ * DBSR_E_ARG), zero padding at the output frame's borders.  `d`
+ * describes the upsampling conv as for dbsr_conv2d (out_mode DBSR_OUT_SHUFFLE, weights packed with shuffle);
+ * y receives the blurred output.  Bitwise equal to the two-call path.  Requires dbsr_conv_shuffle_blur_ok(d):
+ * 16-bit, 1x1 conv cin <= 64 -> 2048 (32 channels x PixelShuffle(8)), low-res frame a multiple of 4 x 4,
+ * NHWC slices aligned to 8 channels. */
+int dbsr_conv_shuffle_blur(const dbsr_conv_desc* d, const float* k9, void* stream);
+int dbsr_conv_shuffle_blur_ok(const dbsr_conv_desc* d);
 /* 1 when dbsr_conv2d_head accepts `d`: pipelined shape (bf16 3x3/s1/p1, width % 64 == 0, height % 8 == 0,
  * >= 256 tiles), cout == 32, residual, act none, post-act ReLU. */
 int dbsr_conv_head_ok(const dbsr_conv_desc* d);

@@ -307,3 +307,39 @@ def test_conv_rejects_slices_past_ld(L):
     d.gate.ld = 72
     assert lib.dbsr_conv2d(d, None) == -1
     assert b'gate slice exceeds ld' in lib.dbsr_last_error()
+
+
+def _shuffle_conv(L, n, h, w, cin, cout=2048, shuffle=8, dtype=None, y_ld=32, y_c0=0):
+    """The decoder's PixelShuffle upsampling conv (1x1 cin -> cout, shuffle), NHWC 16-bit, descriptor only."""
+    dt = L.DBSR_F16 if dtype is None else dtype
+    d = L.ConvDesc()
+    d.n_frames = n
+    cp = 32 if cin <= 32 else 64
+    d.x = L.Tensor(1, dt, h * w * cp, cp, 0, L.FrameMap(1, 1, 0, 1))
+    d.in_h, d.in_w, d.out_h, d.out_w = h, w, h, w
+    d.cin, d.cout, d.kh, d.kw, d.stride, d.pad, d.dil = cin, cout, 1, 1, 1, 0, 1
+    d.w = 1
+    s2 = shuffle * shuffle
+    d.y = L.Tensor(1, dt, h * w * s2 * y_ld, y_ld, y_c0, L.FrameMap(1, 1, 0, 1))
+    d.act = L.ACT_RELU
+    d.res = L.NULL_TENSOR
+    d.gate = L.NULL_TENSOR
+    d.out_mode, d.shuffle = L.OUT_SHUFFLE, shuffle
+    return d
+
+
+def test_shuffle_blur_ok_accepts_and_rejects(L):
+    """dbsr_conv_shuffle_blur_ok (host-only): the decoder's upsampler at the bench shape is served; shapes the fused
+    kernel cannot tile fall back to the two launches (the engine checks _ok first)."""
+    lib = L.lib()
+    ok = lambda d: lib.dbsr_conv_shuffle_blur_ok(ctypes.byref(d))     # noqa: E731
+    assert ok(_shuffle_conv(L, 8, 48, 48, 64)) == 1                  # configs[1]'s decoder
+    assert ok(_shuffle_conv(L, 1, 8, 12, 32, y_ld=48, y_c0=8)) == 1  # cin 32, a channel slice
+    assert ok(_shuffle_conv(L, 8, 47, 48, 64)) == 0                  # low-res height not a multiple of 4
+    assert ok(_shuffle_conv(L, 8, 48, 46, 64)) == 0                  # ... width
+    assert ok(_shuffle_conv(L, 8, 48, 48, 128)) == 0                 # cin > 64 (the weights exceed the registers)
+    assert ok(_shuffle_conv(L, 8, 48, 48, 64, cout=1024)) == 0       # 16 channels per sub-pixel
+    assert ok(_shuffle_conv(L, 8, 48, 48, 64, cout=512, shuffle=4)) == 0
+    assert ok(_shuffle_conv(L, 8, 48, 48, 64, dtype=L.DBSR_F32)) == 0
+    assert ok(_shuffle_conv(L, 8, 48, 48, 64, y_ld=40, y_c0=12)) == 0   # unaligned slice
+    assert ok(_shuffle_conv(L, 8, 48, 48, 64, y_ld=48, y_c0=24)) == 0   # slice past ld
