@@ -24,7 +24,11 @@ typedef __attribute__((ext_vector_type(2))) unsigned int u32x2_t;
 // (tools/isa_audit.py, tests/test_capi.py) -- under-declared VGPR/AGPR counts, LDS-DMA without M0 set in the
 // same basic block, and LDS use beyond the declared group segment.  The audit also fails any future LDS-DMA
 // kernel that does not claim its SIMDs.  Costs nothing at 2 waves per SIMD (their occupancy is already 2).
+#ifndef DBSR_NO_OWN_SIMDS
 #define DBSR_OWN_SIMDS() asm volatile("" ::: "v255")
+#else
+#define DBSR_OWN_SIMDS() do { } while (0)     // (experiment build: LDS-DMA kernels may share their SIMDs)
+#endif
 
 // Barrier after LDS-DMA (buffer/global_load ... lds): every wave first drains its own vector-memory queue, so
 // the pieces it DMA'd have landed before any wave reads them.  __syncthreads() alone does not guarantee this:
@@ -189,6 +193,20 @@ struct StaticFor {
         }
     }
 };
+
+// One 1-KiB LDS-DMA piece issued from inline asm (as conv_wgrad_dma_kernel does): the compiler's wait insertion
+// does not see it, so it neither drains every outstanding piece before the fragment reads (it cannot tell the
+// ring stage being read from the stages being filled) nor at every __syncthreads; the kernel counts its own
+// pieces (vmcnt is in order, so the compiler's own waits only get stricter).  rsrc words: base, stride 0,
+// num_records, raw-buffer flags.
+__device__ __forceinline__ void lds_dma16(const void* base, unsigned bytes, int voff, int soff, unsigned lds_addr) {
+    const unsigned long long a = (unsigned long long)base;
+    typedef int i32x4_t __attribute__((ext_vector_type(4)));
+    const i32x4_t r = {(int)(unsigned)a, (int)((unsigned)(a >> 32) & 0xffffu), (int)bytes, 0x00020000};
+    asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, %3 offen lds" ::"v"(voff), "s"(r), "s"(lds_addr),
+                 "s"(soff)
+                 : "memory", "m0");
+}
 
 }  // namespace dbsr
 

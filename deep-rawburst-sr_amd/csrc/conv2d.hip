@@ -21,6 +21,8 @@
 #include <algorithm>
 #include <type_traits>
 #include <cstdlib>
+#include <cstring>
+#include <vector>
 
 using namespace dbsr;
 
@@ -881,6 +883,12 @@ struct PipeCfg {
 // pixels x 64 B, i.e. 16 cache lines per wave-instruction instead of the 64 of a planar [k-group][pixel]
 // piece, and the swizzle keeps every B-fragment ds_read_b128 conflict-free for any tap shift: within
 // each of its four 16-lane groups, the 4 lanes with equal p mod 4 read 4 distinct phys values.
+// ReLU of two packed 16-bit floats (bf16 or fp16) on their bit patterns: a signed 16-bit max with 0 zeroes every
+// negative value and -0, so relu16x2(pack(x)) == pack(max(x, 0)) bitwise
+__device__ __forceinline__ unsigned relu16x2(unsigned v) {
+    typedef short s16x2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(unsigned, __builtin_elementwise_max(__builtin_bit_cast(s16x2, v), s16x2{0, 0}));
+}
 __device__ __forceinline__ int halo_phys(int p, int g) { return 2 * (g & 1) + ((g >> 1) ^ ((p >> 2) & 1)); }
 
 // Diagnostic build only (make exp EXP_FLAGS=-DDBSR_PIPE_STAMPS): per-wave s_memtime stamps around each
@@ -1667,6 +1675,287 @@ int launch_ws(const ConvK& k, const dbsr_conv_desc* d, int px, hipStream_t s) {
     return 0;
 }
 
+// ------------------------------------------------------------------------------------------------
+// Fused 32-channel ResBlock (blocks.py:81-96: y = relu(x + conv2(relu(conv1(x)))), 3x3/s1/p1 convs with bias):
+// the decoder's 384x384 post-ResBlocks (decoders.py:46-49).  The two ws32 launches it replaces move 377 MB per
+// block at the bench shape (x read twice, the intermediate written and read, y written); this kernel moves
+// x and y once (151 MB) -- the intermediate never leaves the LDS.
+//
+// Persistent blocks of 8 waves (2 per SIMD; one wave per SIMD with 4-group batches measured 87.5 against 62.7
+// us); every wave keeps both convs' weights in registers (A-fragments of the chunk-major pipe copy, 2 x 72
+// VGPRs) and runs 2 pixel groups per MFMA batch with its LDS reads two taps ahead.  Work unit = a 32x16 output tile.  Per tile: the input halo
+// (36 x 20 pixels) arrives by LDS-DMA one tile ahead into a double buffer (the halo_phys swizzle of the
+// weight-stationary kernel; out-of-frame pixels land zeros); conv1 runs on the 34 x 18 intermediate region
+// (39 flattened 16-pixel MFMA groups, 1.2x the output) and writes relu(conv1 + b1), rounded to T -- or zeros
+// outside the frame, conv2's padding -- into an LDS image laid out like the halo; one barrier; conv2 runs on
+// the 32 flattened groups of the tile, adds b2 and the residual (the halo's centre) and stores relu(...).
+// Each output is the arithmetic of conv3x3_ws_kernel's epilogues 1 and 2 (taps in order from 0, bias after,
+// residual after the bias), so the result is bitwise that of the two dbsr_conv2d launches.
+// Block -> tiles: the 256 tiles of a round go to the blocks so that an XCD's 32 blocks take 32 consecutive
+// tiles (their halos overlap in that XCD's L2).
+// ------------------------------------------------------------------------------------------------
+namespace rbk {
+constexpr int TW = 32, TH = 16;
+constexpr int MW = TW + 2, MH = TH + 2, MPX = MW * MH;        // conv1 region 34 x 18
+constexpr int IW = TW + 4, IH = TH + 4, IPX = IW * IH;        // input halo 36 x 20
+constexpr int IN_PIECES = (IPX + 15) / 16;                    // 45 1-KiB pieces
+constexpr int IN_U4 = IN_PIECES * 64;
+constexpr int G1 = (MPX + 15) / 16;                           // 39 conv1 groups
+constexpr int MID_U4 = G1 * 16 * 4;
+constexpr int G2 = TW * TH / 16;                              // 32 conv2 groups
+constexpr int NW = 8;                                         // two waves per SIMD
+constexpr int PER = (IN_PIECES + NW - 1) / NW;                // 6 pieces per wave
+constexpr int Q1 = (G1 + NW - 1) / NW;                        // conv1 groups per wave (5; wave 7: 4)
+constexpr int Q2 = G2 / NW;                                   // conv2 groups per wave (4)
+constexpr int NG = 2;                                         // groups per MFMA batch
+constexpr int LDS_BYTES = (2 * IN_U4 + MID_U4) * 16 + 64 * 4;
+static_assert(LDS_BYTES <= 160 * 1024, "resblock LDS");
+}  // namespace rbk
+
+// tile of block b's round i (blocks b < ntiles % nb take one round more): a full round of 256 tiles goes to the
+// 256 blocks so that XCD b % 8 takes 32 consecutive tiles; a partial last round in block order (its tiles exist
+// only for b < ntiles % nb -- applied to it, the XCD order addressed tiles past the last frame)
+__host__ __device__ __forceinline__ int rb_tile(int i, int b, int nb, int ntiles) {
+    if (nb == 256 && (i + 1) * 256 <= ntiles) return i * 256 + (b & 7) * 32 + (b >> 3);
+    return i * nb + b;
+}
+
+template <typename T>
+__global__ __launch_bounds__(512, 1) void resblock32_kernel(ConvK k1, ConvK k2, int tiles_x, int tiles_y,
+                                                            int ntiles) {
+    using namespace rbk;
+    DBSR_OWN_SIMDS();
+    __shared__ __attribute__((aligned(16))) u32x4_t lds[2 * IN_U4 + MID_U4 + 16];
+    u32x4_t* lmid = lds + 2 * IN_U4;
+    float* lbias = (float*)(lds + 2 * IN_U4 + MID_U4);            // [b1 (32)][b2 (32)]
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int H = k1.in_h, W = k1.in_w;
+
+    // both convs' A-fragments: piece (half h, tap) of the chunk-major copy is lane-major 1 KiB
+    Frag<T> w1[9][2], w2[9][2];
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            w1[tap][h].load((const T*)((const char*)k1.w_pipe + (h * 9 + tap) * 1024 + lane * 16));
+            w2[tap][h].load((const T*)((const char*)k2.w_pipe + (h * 9 + tap) * 1024 + lane * 16));
+        }
+    if (threadIdx.x < 64) {
+        const ConvK& kb = threadIdx.x < 32 ? k1 : k2;
+        lbias[threadIdx.x] = kb.bias ? kb.bias[threadIdx.x & 31] : 0.f;
+    }
+
+    struct Tile { const T* xf; long long y_off; int y0, x0; };
+    auto decode = [&](int i) {
+        const int t = rb_tile(i, blockIdx.x, gridDim.x, ntiles);
+        Tile tl;
+        const int tx = t % tiles_x, r = t / tiles_x, ty = r % tiles_y, f = r / tiles_y;
+        tl.y0 = ty * TH; tl.x0 = tx * TW;
+        tl.xf = (const T*)k1.x + map_frame(k1.xm, f) * k1.x_is;
+        tl.y_off = map_frame(k2.ym, f) * k2.y_is + k2.y_c0 + ((long long)tl.y0 * W + tl.x0) * k2.y_ld;
+        return tl;
+    };
+    const int my_tiles = ntiles / (int)gridDim.x + ((int)blockIdx.x < ntiles % (int)gridDim.x ? 1 : 0);
+    const int pix_b = k1.x_ld * (int)sizeof(T);
+    const unsigned frame_bytes = (unsigned)((long long)H * W * pix_b);
+    const unsigned lds0 = (unsigned)(unsigned long long)(__attribute__((address_space(3))) u32x4_t*)lds;
+    // the next tile's halo: inline-asm LDS-DMA (lds_dma16), so the compiler does not drain it before the conv1
+    // epilogue's LDS writes; the drain is the vm_drain of the tile's second barrier
+    auto dma = [&](const Tile& tl, int buf) {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+#pragma unroll
+        for (int it = 0; it < PER; ++it) {
+            const int piece = min(wave + NW * it, IN_PIECES - 1);
+            const int p = piece * 16 + (ln >> 2), ph = ln & 3;
+            const int gg = 2 * ((ph & 1) ^ ((p >> 2) & 1)) + (ph >> 1);
+            const int r = p / IW, c = p - r * IW;
+            const int hy = tl.y0 - 2 + r, hx = tl.x0 - 2 + c;
+            const bool ok = p < IPX && (unsigned)hy < (unsigned)H && (unsigned)hx < (unsigned)W;
+            lds_dma16(tl.xf, frame_bytes, ok ? (hy * W + hx) * pix_b + gg * 16 : BUF_OOB, 0,
+                      lds0 + (buf * IN_U4 + piece * 64) * 16);
+        }
+    };
+
+    // the 9 taps of NG 16-pixel groups (image rows iw wide, group j's tap-(0,0) pixel P0[j]): B-fragments read
+    // two taps ahead (a 3-deep ring per group)
+    auto taps = [&](const u32x4_t* img, int iw, int g, const int (&P0)[NG], const Frag<T> (&w)[9][2],
+                    f32x4_t (&acc)[NG][2]) {
+        int bs[NG][8];
+#pragma unroll
+        for (int j = 0; j < NG; ++j)
+#pragma unroll
+            for (int rho = 0; rho < 8; ++rho) bs[j][rho] = 4 * P0[j] + halo_phys(P0[j] + rho, g);
+        Frag<T> bq[NG][3];
+        auto rd = [&](int j, int tap) {
+            const int imm = (tap / 3) * iw + tap % 3;
+            Frag<T> b;
+            b.v = __builtin_bit_cast(bf16x8_t, img[bs[j][imm & 7] + 4 * imm]);
+            return b;
+        };
+#pragma unroll
+        for (int j = 0; j < NG; ++j) {
+            bq[j][0] = rd(j, 0);
+            bq[j][1] = rd(j, 1);
+        }
+        StaticFor<0, 9>::run([&](auto t_) {
+            constexpr int tap = decltype(t_)::value;
+            const f32x4_t z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int j = 0; j < NG; ++j) {
+                acc[j][0] = mma(w[tap][0], bq[j][tap % 3], tap == 0 ? z : acc[j][0]);
+                acc[j][1] = mma(w[tap][1], bq[j][tap % 3], tap == 0 ? z : acc[j][1]);
+                if constexpr (tap + 2 < 9) bq[j][(tap + 2) % 3] = rd(j, tap + 2);
+            }
+        });
+        // the scheduler's MFMA / DS-read interleave for small GEMM loops: without it the reads sank to their uses
+        // and every tap waited on its own read (measured: 69-71 us either way, two launches 75 us)
+        __builtin_amdgcn_iglp_opt(0);
+    };
+
+    Tile cur = decode(0), prev = cur;
+    if (my_tiles > 0) dma(cur, 0);
+    u32x4_t outv[Q2];                   // the previous tile's conv2 outputs, stored after this tile's first barrier
+    for (int ti = 0; ti < my_tiles; ++ti) {
+        dma_barrier();                  // B0: tile ti's halo landed; the intermediate image is free
+        // lane-derived values recomputed per tile from an opaque copy of the lane index (hoisted out of the loop,
+        // the groups' per-lane LDS bases took registers for the whole loop)
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const int g = ln >> 4, col = ln & 15;
+        if (ti > 0) {
+#pragma unroll
+            for (int i = 0; i < Q2; ++i) {
+                const int q = wave + NW * i;
+                *(u32x4_t*)((T*)k2.y + prev.y_off + ((long long)(q >> 1) * W + 16 * (q & 1) + col) * k2.y_ld + 8 * g) =
+                    outv[i];
+            }
+        }
+        const u32x4_t* lin = lds + (ti & 1) * IN_U4;
+        const bool more = ti + 1 < my_tiles;
+        const Tile nxt = more ? decode(ti + 1) : cur;
+        if (more) dma(nxt, (ti + 1) & 1);
+        // ---- conv1 on the intermediate region: groups wave + 4 i, in batches of NG ----
+        {
+            const float4 b0 = *(const float4*)(lbias + 8 * g), b1 = *(const float4*)(lbias + 8 * g + 4);
+            const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+            StaticFor<0, (Q1 + NG - 1) / NG>::run([&](auto bt_) {
+                constexpr int bt = decltype(bt_)::value;
+                int pa[NG], P0[NG];
+#pragma unroll
+                for (int j = 0; j < NG; ++j) {
+                    pa[j] = min(16 * (wave + NW * (NG * bt + j)) + col, MPX - 1);
+                    const int r = pa[j] / MW, c = pa[j] - r * MW;
+                    P0[j] = r * IW + c;
+                }
+                f32x4_t acc[NG][2];
+                taps(lin, IW, g, P0, w1, acc);
+#pragma unroll
+                for (int j = 0; j < NG; ++j) {
+                    const int p = 16 * (wave + NW * (NG * bt + j)) + col;
+                    const int r = pa[j] / MW, c = pa[j] - r * MW;
+                    const int fy = cur.y0 - 1 + r, fx = cur.x0 - 1 + c;
+                    const bool inside = (unsigned)fy < (unsigned)H && (unsigned)fx < (unsigned)W;
+                    u32x4_t o;
+#pragma unroll
+                    for (int e = 0; e < 2; ++e) {
+                        o[e] = relu16x2(H16<T>::pack(acc[j][0][2 * e] + bv[2 * e], acc[j][0][2 * e + 1] + bv[2 * e + 1]));
+                        o[2 + e] = relu16x2(H16<T>::pack(acc[j][1][2 * e] + bv[4 + 2 * e],
+                                                         acc[j][1][2 * e + 1] + bv[4 + 2 * e + 1]));
+                    }
+                    if (!inside) o = u32x4_t{0u, 0u, 0u, 0u};
+                    if (p < MPX) lmid[4 * p + halo_phys(p, g)] = o;
+                }
+            });
+        }
+        dma_barrier();                  // B1: the intermediate image is complete (the next halo's DMA, issued before
+                                        // conv1, has landed too: no LDS-DMA crosses a barrier in flight)
+        // ---- conv2 on the tile: groups wave + 4 i, in batches of NG ----
+        {
+            const float4 b0 = *(const float4*)(lbias + 32 + 8 * g), b1 = *(const float4*)(lbias + 32 + 8 * g + 4);
+            const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+            StaticFor<0, Q2 / NG>::run([&](auto bt_) {
+                constexpr int bt = decltype(bt_)::value;
+                int row[NG], cc[NG], P0[NG];
+#pragma unroll
+                for (int j = 0; j < NG; ++j) {
+                    const int q = wave + NW * (NG * bt + j);
+                    row[j] = q >> 1;
+                    cc[j] = 16 * (q & 1) + col;
+                    P0[j] = row[j] * MW + cc[j];
+                }
+                f32x4_t acc[NG][2];
+                taps(lmid, MW, g, P0, w2, acc);
+#pragma unroll
+                for (int j = 0; j < NG; ++j) {
+                    const int PR = (row[j] + 2) * IW + cc[j] + 2;
+                    const u32x4_t rq = lin[4 * PR + halo_phys(PR, g)];
+                    float v[8];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        v[r] = acc[j][0][r] + bv[r];
+                        v[4 + r] = acc[j][1][r] + bv[4 + r];
+                    }
+                    u32x4_t o;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        o[e] = relu16x2(H16<T>::pack(v[2 * e] + H16<T>::lo(rq[e]), v[2 * e + 1] + H16<T>::hi(rq[e])));
+                    outv[NG * bt + j] = o;
+                }
+            });
+        }
+        prev = cur;
+        cur = nxt;
+    }
+    if (my_tiles > 0) {
+        const int g = lane >> 4, col = lane & 15;
+#pragma unroll
+        for (int i = 0; i < Q2; ++i) {
+            const int q = wave + NW * i;
+            *(u32x4_t*)((T*)k2.y + prev.y_off + ((long long)(q >> 1) * W + 16 * (q & 1) + col) * k2.y_ld + 8 * g) = outv[i];
+        }
+    }
+    vm_drain();                         // (no LDS-DMA outstanding at s_endpgm: tools/isa_audit.py)
+}
+
+// every (block, round) of a launch maps to a distinct tile below ntiles (checked on the host before each launch)
+bool rb_mapping_ok(int nb, int ntiles) {
+    std::vector<unsigned char> seen(ntiles, 0);
+    for (int b = 0; b < nb; ++b) {
+        const int my = ntiles / nb + (b < ntiles % nb ? 1 : 0);
+        for (int i = 0; i < my; ++i) {
+            const int t = rb_tile(i, b, nb, ntiles);
+            if (t < 0 || t >= ntiles || seen[t]) return false;
+            seen[t] = 1;
+        }
+    }
+    return true;
+}
+
+// the fused ResBlock applies: c1 = conv1 (x -> any, ReLU), c2 = conv2 (-> y, residual x, post-ReLU), both
+// 16-bit 3x3/s1/p1/d1 32 -> 32 with chunk-major weight copies, frames a multiple of 32 x 16, NHWC slices aligned
+bool use_resblock32(const dbsr_conv_desc* c1, const dbsr_conv_desc* c2) {
+    auto conv_ok = [](const dbsr_conv_desc* d) {
+        return is16(d->x.dtype) && d->y.dtype == d->x.dtype && !d->precise && d->kh == 3 && d->kw == 3 &&
+               d->stride == 1 && d->pad == 1 && d->dil == 1 && d->cin == 32 && d->cout == 32 &&
+               d->out_mode == DBSR_OUT_NHWC && !d->gate.ptr && d->in_h == d->out_h && d->in_w == d->out_w;
+    };
+    if (!c1 || !c2 || !conv_ok(c1) || !conv_ok(c2)) return false;
+    if (c1->act != DBSR_ACT_RELU || c1->res.ptr || c2->act != DBSR_ACT_NONE || c2->post_act != DBSR_ACT_RELU)
+        return false;
+    // the residual is conv1's input (same tensor, slice and frames)
+    if (c2->res.ptr != c1->x.ptr || c2->res.c0 != c1->x.c0 || c2->res.ld != c1->x.ld ||
+        c2->res.img_stride != c1->x.img_stride || c2->res.dtype != c1->x.dtype ||
+        std::memcmp(&c2->res.map, &c1->x.map, sizeof(dbsr_frame_map)) != 0)
+        return false;
+    if (c1->n_frames != c2->n_frames || c1->in_h != c2->in_h || c1->in_w != c2->in_w || c1->x.dtype != c2->y.dtype)
+        return false;
+    if (c1->in_w % rbk::TW || c1->in_h % rbk::TH) return false;
+    if (c1->x.ld % 8 || c1->x.c0 % 8 || c1->x.c0 + 32 > c1->x.ld) return false;
+    if (c2->y.ld % 8 || c2->y.c0 % 8 || c2->y.c0 + 32 > c2->y.ld) return false;
+    return (long long)c1->in_h * c1->in_w * c1->x.ld * 2 < (1LL << 31);
+}
+
 template <typename T>
 int dispatch_ws(int px, const ConvK& k, const dbsr_conv_desc* d, const dbsr_conv_desc* sel, hipStream_t s) {
     if (ws_narrow(sel)) return launch_ws<T, 32, 64, 8, 1>(k, d, px, s);
@@ -1975,12 +2264,6 @@ int launch_upsample(const ConvK& k, hipStream_t s) {
 #ifndef DBSR_UB_ABL
 #define DBSR_UB_ABL 0        // timing-only ablations: 1 no conv phase, 2 no blur phase, 4 no blur stores
 #endif
-// ReLU of two packed 16-bit floats (bf16 or fp16) on their bit patterns: a signed 16-bit max with 0 zeroes every
-// negative value and -0, so relu16x2(pack(x)) == pack(max(x, 0)) bitwise
-__device__ __forceinline__ unsigned relu16x2(unsigned v) {
-    typedef short s16x2 __attribute__((ext_vector_type(2)));
-    return __builtin_bit_cast(unsigned, __builtin_elementwise_max(__builtin_bit_cast(s16x2, v), s16x2{0, 0}));
-}
 namespace ub {
 constexpr int LT = 4, S = 8, HS = LT * S + 2, NPX = HS * HS;      // image: HS x HS pixels
 constexpr int IMG_U2 = NPX * 8;                                   // ... in 8-B units
@@ -2599,6 +2882,30 @@ extern "C" int dbsr_conv2d(const dbsr_conv_desc* d, void* stream) {
     if (use_pointwise(sel)) return d->x.dtype == DBSR_F16 ? launch_pointwise<f16_t>(k, s) : launch_pointwise<bf16_t>(k, s);
     if (d->x.dtype == DBSR_F16) return dispatch_conv<f16_t>(k, d, sel, s);
     return d->x.dtype == DBSR_BF16 ? dispatch_conv<bf16_t>(k, d, sel, s) : dispatch_conv<float>(k, d, sel, s);
+}
+
+extern "C" int dbsr_resblock_ok(const dbsr_conv_desc* c1, const dbsr_conv_desc* c2) {
+    return use_resblock32(c1, c2) ? 1 : 0;
+}
+
+extern "C" int dbsr_resblock(const dbsr_conv_desc* c1, const dbsr_conv_desc* c2, void* stream) {
+    DBSR_CHECK_ARG(c1 && c2 && c1->x.ptr && c1->w && c2->w && c2->y.ptr, "resblock: null pointer");
+    DBSR_CHECK_ARG(c1->x.map.fpg > 0 && c2->y.map.fpg > 0 && c1->n_frames > 0, "resblock: bad frame map / sizes");
+    DBSR_CHECK_ARG(use_resblock32(c1, c2), "resblock: needs two 16-bit 3x3/s1/p1 32 -> 32 convs (conv1 ReLU; conv2 "
+                   "residual = conv1's input, post-ReLU), frames a multiple of 32 x 16, NHWC slices aligned to 8");
+    const ConvK k1 = make_convk(c1), k2 = make_convk(c2);
+    const int tiles_x = c1->in_w / rbk::TW, tiles_y = c1->in_h / rbk::TH;
+    const int ntiles = c1->n_frames * tiles_x * tiles_y;
+    int grid = c1->max_blocks > 0 ? std::min(c1->max_blocks, num_cus()) : num_cus();
+    grid = std::min(grid, ntiles);
+    DBSR_CHECK_ARG(rb_mapping_ok(grid, ntiles), "resblock: tile mapping out of range (grid %d, %d tiles)", grid, ntiles);
+    hipStream_t s = (hipStream_t)stream;
+    if (c1->x.dtype == DBSR_F16)
+        hipLaunchKernelGGL(resblock32_kernel<f16_t>, dim3(grid), dim3(512), 0, s, k1, k2, tiles_x, tiles_y, ntiles);
+    else
+        hipLaunchKernelGGL(resblock32_kernel<bf16_t>, dim3(grid), dim3(512), 0, s, k1, k2, tiles_x, tiles_y, ntiles);
+    DBSR_LAUNCH_CHECK();
+    return 0;
 }
 
 extern "C" int dbsr_conv_shuffle_blur_ok(const dbsr_conv_desc* d) { return use_upsample_blur(d) ? 1 : 0; }

@@ -58,19 +58,6 @@ __device__ __forceinline__ f32x4_t mfma16(const bf16x8_t& a, const bf16x8_t& b, 
                                                       0, 0, 0);
 }
 
-// One 1-KiB LDS-DMA piece issued from inline asm (as conv_wgrad_dma_kernel does): the compiler's wait insertion
-// does not see it, so it neither drains every outstanding piece before the fragment reads (it cannot tell the
-// ring stage being read from the stages being filled) nor at every __syncthreads; the kernel counts its own
-// pieces (vmcnt is in order, so the compiler's own waits only get stricter).  rsrc words: base, stride 0,
-// num_records, raw-buffer flags.
-__device__ __forceinline__ void fz_dma(const void* base, unsigned bytes, int voff, int soff, unsigned lds_addr) {
-    const unsigned long long a = (unsigned long long)base;
-    typedef int i32x4_t __attribute__((ext_vector_type(4)));
-    const i32x4_t r = {(int)(unsigned)a, (int)((unsigned)(a >> 32) & 0xffffu), (int)bytes, 0x00020000};
-    asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, %3 offen lds" ::"v"(voff), "s"(r), "s"(lds_addr),
-                 "s"(soff)
-                 : "memory", "m0");
-}
 
 // pixel-major halo image of one 32-channel chunk: halo pixel p's 4 k-groups at slots 4p..4p+3, k-group g
 // at 4p + phys(p, g) (the pipelined conv kernel's swizzle: conflict-free ds_read_b128 for every tap shift)
@@ -165,7 +152,7 @@ __global__ __launch_bounds__(512, 1) void conv_fuse_kernel(FuseK k, int tiles_x,
         if (item < C::W_ITEMS) {
             const int kx = item / (C::WM / 16), b16 = item % (C::WM / 16);
             const int piece = (((t.cb >> 4) + b16) * k.nchunks + c) * 9 + 3 * ky + kx;
-            fz_dma(k.w_pipe, 0xffffffffu, lane * 16, piece * 1024, lds0 + (wb * C::W_U4 + item * 64) * 16);
+            lds_dma16(k.w_pipe, 0xffffffffu, lane * 16, piece * 1024, lds0 + (wb * C::W_U4 + item * 64) * 16);
         } else {
             const int ri = item - C::W_ITEMS;
             const int r = (ky == 0 ? 0 : ky + 1) + ri / C::RP, j = ri % C::RP;
@@ -177,7 +164,7 @@ __global__ __launch_bounds__(512, 1) void conv_fuse_kernel(FuseK k, int tiles_x,
             const int n = p / C::HWD, cc = p - n * C::HWD;
             const int hy = t.y0 - 1 + r, hx = t.x0 - 1 + cc;
             const bool ok = p < C::ROW_PX && (unsigned)hy < (unsigned)k.H && (unsigned)hx < (unsigned)k.W;
-            fz_dma((const T*)k.x + t.bb * k.x_b, k.x_span,
+            lds_dma16((const T*)k.x + t.bb * k.x_b, k.x_span,
                    ok ? n * k.x_nb + (hy * k.W + hx) * pix_b + c * 64 + gg * 16 : BUF_OOB, 0,
                    lds0 + (C::ROWS_OFF + slot * C::ROW_U4 + j * 64) * 16);
         }

@@ -283,6 +283,22 @@ class Plan:
         self.kernel[len(self.ops) - 1] = 'conv_fuse'
         return len(self.ops) - 1
 
+    def resblock(self, name, c1, c2, n_frames, x, mid, y, hw):
+        """ResBlock (blocks.py:81-96) x -> y as one launch (dbsr_resblock: the intermediate stays in the LDS) when
+        the library serves it; returns False otherwise (the caller then emits conv1 into `mid` and conv2)."""
+        d1 = self._desc(name + '.conv1', c1, n_frames, x, 0, hw, mid, 0, L.ACT_RELU, IDENTITY, IDENTITY, None, 0,
+                        IDENTITY, L.ACT_NONE, L.OUT_NHWC, 0, None, None, False, None, 0, IDENTITY)
+        d2 = self._desc(name + '.conv2', c2, n_frames, mid, 0, hw, y, 0, L.ACT_NONE, IDENTITY, IDENTITY, x, 0,
+                        IDENTITY, L.ACT_RELU, L.OUT_NHWC, 0, None, None, False, None, 0, IDENTITY)
+        if not L.lib().dbsr_resblock_ok(ctypes.byref(d1), ctypes.byref(d2)):
+            return False
+        self.convs.extend([(d1, self.lane), (d2, self.lane)])
+        oh, ow = d1.out_h, d1.out_w
+        flop = 2.0 * n_frames * oh * ow * (c1.cout * d1.cin * 9 + c2.cout * d2.cin * 9)
+        self.add(name, L.lib().dbsr_resblock, ctypes.byref(d1), ctypes.byref(d2), work=('flop', flop))
+        self.kernel[len(self.ops) - 1] = 'resblock32'
+        return True
+
     def conv_shuffle_blur(self, name, pc, n_frames, x, in_hw, y, act, k9):
         """The PixelShuffle upsampler's conv + shuffle + 3x3 Gaussian blur in one launch
         (dbsr_conv_shuffle_blur: the pre-blur tensor never reaches memory; upsampling.py:51-66).  Returns the
@@ -631,6 +647,8 @@ class DBSREngine:
     FUSED_HEAD = True
     # PixelShuffle upsampler conv + shuffle + blur in one kernel (dbsr_conv_shuffle_blur)
     FUSED_UPSAMPLE_BLUR = True
+    # 32-channel ResBlocks (the decoder's post blocks) as one kernel each (dbsr_resblock)
+    FUSED_RESBLOCK = True
     # weight-predictor input conv split into a per-frame [proj, offfeat] conv + a per-burst base conv
     LINEAR_SPLIT = True
     # weight-predictor output conv + softmax + fusion in one kernel (dbsr_conv_fuse_softmax: the fp32 logits never
@@ -730,6 +748,11 @@ class DBSREngine:
         fused = False
         for i, (c1, c2) in enumerate(blocks):
             b, c = [j for j in range(3) if j != a]
+            last_head = head is not None and i == len(blocks) - 1
+            if DBSREngine.FUSED_RESBLOCK and not last_head and \
+                    plan.resblock(f'{name}{i}', c1, c2, n, bufs[a], bufs[b], bufs[c], hw):
+                a = c
+                continue
             plan.conv(f'{name}{i}.conv1', c1, n, bufs[a], 0, hw, bufs[b], 0, L.ACT_RELU)
             d = plan.conv(f'{name}{i}.conv2', c2, n, bufs[b], 0, hw, bufs[c], 0, L.ACT_NONE, res=bufs[a],
                           post_act=L.ACT_RELU, head=head if i == len(blocks) - 1 else None)

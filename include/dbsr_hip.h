@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define DBSR_ABI_VERSION 16
+#define DBSR_ABI_VERSION 17
 
 enum { DBSR_F32 = 0, DBSR_BF16 = 1, DBSR_F16 = 2 };
 enum { DBSR_ACT_NONE = 0, DBSR_ACT_RELU = 1, DBSR_ACT_LRELU = 2 };      /* LeakyReLU slope 0.1 */
@@ -149,6 +149,14 @@ int dbsr_conv2d_head(const dbsr_conv_desc* d, const float* head_w, const float* 
  * NHWC slices aligned to 8 channels. */
 int dbsr_conv_shuffle_blur(const dbsr_conv_desc* d, const float* k9, void* stream);
 int dbsr_conv_shuffle_blur_ok(const dbsr_conv_desc* d);
+/* A whole 32-channel ResBlock in one launch (ABI 17; blocks.py:81-96, replaces the pair of dbsr_conv2d calls of
+ * a decoder post-ResBlock, decoders.py:46-49): y = relu(x + conv2(relu(conv1(x)))).  c1 = conv1 as for dbsr_conv2d
+ * (x -> its y, act ReLU), c2 = conv2 (its x, y, residual = c1's input, act none, post-act ReLU); c1->y and c2->x
+ * name the intermediate, which this call neither reads nor writes (it stays on chip).  Bitwise equal to the two
+ * calls.  Requires dbsr_resblock_ok(c1, c2): 16-bit 3x3/s1/p1 convs 32 -> 32, frames a multiple of 32 x 16,
+ * NHWC slices aligned to 8 channels; c1->max_blocks caps the persistent grid. */
+int dbsr_resblock(const dbsr_conv_desc* c1, const dbsr_conv_desc* c2, void* stream);
+int dbsr_resblock_ok(const dbsr_conv_desc* c1, const dbsr_conv_desc* c2);
 /* 1 when dbsr_conv2d_head accepts `d`: pipelined shape (bf16 3x3/s1/p1, width % 64 == 0, height % 8 == 0,
  * >= 256 tiles), cout == 32, residual, act none, post-act ReLU. */
 int dbsr_conv_head_ok(const dbsr_conv_desc* d);

@@ -237,7 +237,9 @@ def test_conv2d_head_rejects_ineligible(ops):
 def test_conv1x1_pixelshuffle(ops, case):
     """PixelShuffle upsampler (1x1 conv + ReLU + shuffle, upsampling.py:51-66): the dedicated bf16 kernel
     (dbsr_conv_kernel_for == 3) against torch on the same bf16-rounded operands and against the generic
-    kernel's shuffle epilogue (algo 0)."""
+    kernel's shuffle epilogue (algo 0).  The dedicated kernel starts its accumulators at the bias (the order
+    dbsr_conv_shuffle_blur shares), the generic kernel adds the bias after the K sum: one fp32 rounding apart,
+    so at most one bf16 rounding step (rtol 2^-7)."""
     from dbsr_amd import _lib
     N, Cin, H, W, s = case
     Cout = 32 * s * s
@@ -257,7 +259,7 @@ def test_conv1x1_pixelshuffle(ops, case):
         _lib.lib().dbsr_set_conv_algo(2)
     assert outs[2].shape == ref.shape
     np.testing.assert_allclose(outs[2].numpy(), ref.numpy(), atol=2e-2, rtol=1e-2)
-    np.testing.assert_array_equal(outs[2].numpy(), outs[0].numpy())
+    np.testing.assert_allclose(outs[2].numpy(), outs[0].numpy(), rtol=2.0 ** -7, atol=1e-6)
 
 
 @pytest.mark.parametrize('case', [(2, 512, 64, 48, 48, torch.bfloat16, 1, True),    # merge projection shape
@@ -327,7 +329,9 @@ def test_conv3x3_narrow(ops, dt, case):
 @pytest.mark.parametrize('shape', [(2, 32, 384, 384), (1, 16, 13, 21), (3, 8, 9, 4)])
 def test_gauss_blur3(shape, dt):
     """Sliding-window 3x3 Gaussian (upsampling.py:59-65, filtering.py:29-40) against the oracle's blur
-    (16-bit: on the rounded input, fp32 sums, one rounding of the output)."""
+    (16-bit: on the rounded input, fp32 sums, one rounding of the output).  The 16-bit kernel sums the separable
+    pair (blur_row / blur_col) where torch sums the 9 taps: the fp32 sums differ by roundings, which can move the
+    16-bit output by one rounding step (rtol 2 ulps of the dtype)."""
     from dbsr_amd import _lib as L
     N, C, H, W = shape
     x = torch.randn(N, C, H, W, generator=torch.Generator().manual_seed(H + W + C)).to(dt).float()
@@ -341,5 +345,5 @@ def test_gauss_blur3(shape, dt):
     kb = (ctypes.c_float * 9)(*kern.flatten().tolist())
     L.check(L.lib().dbsr_gauss_blur3(N, H, W, C, L.tensor_desc(xs, C), kb, L.tensor_desc(out, C),
                                      L.stream_ptr(xs.device)), 'blur')
-    tol = 1e-5 if dt == torch.float32 else (2 ** -8 if dt == torch.bfloat16 else 2 ** -11)
+    tol = 1e-5 if dt == torch.float32 else (2 ** -7 if dt == torch.bfloat16 else 2 ** -10)
     np.testing.assert_allclose(out.permute(0, 3, 1, 2).float().cpu().numpy(), ref.numpy(), atol=1e-5, rtol=tol)

@@ -1,0 +1,113 @@
+"""dbsr_resblock: a whole 32-channel ResBlock (models/layers/blocks.py:81-96, the decoder's post blocks of
+decoders.py:46-49) in one kernel, against the two dbsr_conv2d launches it replaces -- bitwise: both convs sum their
+taps in the weight-stationary kernel's order, add the bias after the taps and the residual after the bias, and the
+intermediate is rounded to the activation dtype exactly as the first launch stores it -- and against torch on the
+same 16-bit operands (fp32 convs, the intermediate rounded to the dtype: atol 2e-2 + rtol 2 quanta)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+DEV = 'cuda'
+pytestmark = pytest.mark.gpu
+
+
+class _Slice:
+    def __init__(self, t, c0):
+        self.nhwc, self.c0 = t, c0
+
+    def d(self, c0=0, fmap=None):
+        return self.nhwc.d(self.c0 + c0) if fmap is None else self.nhwc.d(self.c0 + c0, fmap)
+
+
+def _run(B, H, W, dt, seed, y_ld=32, y_c0=0, x_ld=32, x_c0=0):
+    from dbsr_amd import _lib as L
+    from dbsr_amd.engine import NHWC, PackedConv, Plan
+    gen = torch.Generator().manual_seed(seed)
+    x = torch.randn(B, 32, H, W, generator=gen)
+    convs = []
+    for _ in range(2):
+        c = torch.nn.Conv2d(32, 32, 3, padding=1)
+        with torch.no_grad():
+            c.weight.copy_(torch.randn(32, 32, 3, 3, generator=gen) * (2.0 / 288) ** 0.5)
+            c.bias.copy_(torch.randn(32, generator=gen) * 0.1)
+        convs.append(c)
+    dev = torch.device(DEV)
+    s = torch.cuda.current_stream().cuda_stream
+    pcs = [PackedConv(c.to(dev), dt, dev, s) for c in convs]
+    X = NHWC(B, H, W, x_ld, dt, dev)
+    X.t[..., x_c0:x_c0 + 32].copy_(x.permute(0, 2, 3, 1).to(dt))
+    Xs = _Slice(X, x_c0)
+    outs = {}
+    for fused in (True, False):
+        Y = NHWC(B, H, W, y_ld, dt, dev)
+        Y.t.fill_(7.0)                                  # channels outside the slice stay untouched
+        M = NHWC(B, H, W, 32, dt, dev)
+        plan = Plan()
+        if fused:
+            assert plan.resblock('rb', pcs[0], pcs[1], B, Xs, M, _Slice(Y, y_c0), (H, W)), 'dbsr_resblock_ok rejected'
+        else:
+            plan.conv('c1', pcs[0], B, Xs, 0, (H, W), M, 0, L.ACT_RELU)
+            plan.conv('c2', pcs[1], B, M, 0, (H, W), _Slice(Y, y_c0), 0, L.ACT_NONE, res=Xs, post_act=L.ACT_RELU)
+        plan.finalize_workspace(dev)
+        plan.run(s)
+        torch.cuda.synchronize()
+        outs[fused] = Y.t.cpu()
+        if not fused:
+            outs['kernels'] = set(plan.kernel.values())
+    xb = x.to(dt).float()
+    w = [c.weight.detach().cpu().to(dt).float() for c in convs]
+    b = [c.bias.detach().cpu() for c in convs]
+    mid = F.relu(F.conv2d(xb, w[0], b[0], padding=1)).to(dt).float()
+    ref = F.relu(F.conv2d(mid, w[1], b[1], padding=1) + xb)
+    return outs, ref.permute(0, 2, 3, 1)
+
+
+@pytest.mark.parametrize('case', [(8, 384, 384, torch.float16, 32, 0, 32, 0),   # the bench decoder's post blocks
+                                  (4, 128, 128, torch.bfloat16, 32, 0, 32, 0),
+                                  (1, 384, 384, torch.float16, 32, 0, 32, 0),  # 288 tiles: a partial last round
+                                  (3, 256, 256, torch.bfloat16, 32, 0, 32, 0), # 384 tiles
+                                  (8, 64, 128, torch.float16, 48, 8, 40, 8),   # channel slices of x and y
+                                  (1, 16, 32, torch.float16, 48, 8, 40, 8),    # one tile per frame
+                                  (3, 48, 64, torch.bfloat16, 40, 0, 48, 16)])
+def test_resblock_vs_two_convs_and_torch(case):
+    B, H, W, dt, y_ld, y_c0, x_ld, x_c0 = case
+    outs, ref = _run(B, H, W, dt, seed=B * 100 + H + W, y_ld=y_ld, y_c0=y_c0, x_ld=x_ld, x_c0=x_c0)
+    f, t = outs[True], outs[False]
+    nd = int((f.view(torch.int16) != t.view(torch.int16)).sum())
+    if outs['kernels'] == {'conv3x3_ws'}:
+        # the two launches ran the weight-stationary kernel, whose summation order the fused kernel keeps
+        assert nd == 0, 'fused ResBlock differs from the two dbsr_conv2d launches at %d elements' % nd
+    else:
+        # (small frames dispatch the two launches to another kernel: same sums in another order)
+        np.testing.assert_allclose(f.float().numpy(), t.float().numpy(), atol=1e-2, rtol=1e-2)
+    if y_ld > 32:
+        mask = torch.ones(y_ld, dtype=torch.bool)
+        mask[y_c0:y_c0 + 32] = False
+        assert torch.all(f[..., mask].float() == 7.0)
+    eps = 2.0 ** -8 if dt == torch.bfloat16 else 2.0 ** -11
+    np.testing.assert_allclose(f[..., y_c0:y_c0 + 32].float().numpy(), ref.numpy(), atol=2e-2, rtol=2 * eps)
+
+
+def test_resblock_in_engine_matches_unfused():
+    """The DBSR forward (configs[1]'s architecture, seeded random weights, 24x24 bursts: 192x192 decoder frames)
+    with DBSREngine.FUSED_RESBLOCK on and off: bitwise equal predictions."""
+    import dbsr_amd
+    from dbsr_amd.engine import DBSREngine
+    torch.manual_seed(0)
+    sd = dbsr_amd.dbsrnet_cvpr2021(**dbsr_amd.DBSR_SYNTHETIC_KWARGS).state_dict()
+    burst = torch.rand(2, 14, 4, 24, 24)
+    outs = []
+    old = DBSREngine.FUSED_RESBLOCK
+    try:
+        for flag in (True, False):
+            DBSREngine.FUSED_RESBLOCK = flag
+            net = dbsr_amd.dbsrnet_cvpr2021(**dbsr_amd.DBSR_SYNTHETIC_KWARGS)
+            net.load_state_dict(sd)
+            net = net.to(DEV).eval().set_compute_dtype(torch.float16)
+            with torch.no_grad():
+                pred, _ = net(burst.to(DEV))
+            outs.append(pred.float().cpu())
+    finally:
+        DBSREngine.FUSED_RESBLOCK = old
+    assert torch.equal(outs[0], outs[1])

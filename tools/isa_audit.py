@@ -6,7 +6,10 @@ race'): every kernel that issues LDS-DMA (buffer_load_* ... lds / glo
     wave of another kernel (another stream's) can be co-resident on those SIMDs (DBSR_OWN_SIMDS);
   * set M0 (the LDS-DMA destination base) in the same basic block before every LDS-DMA instruction;
   * declare at least as many registers as its code uses (highest v/a register index in the ISA);
-  * stay within its declared LDS (.group_segment_fixed_size <= 160 KiB).
+  * stay within its declared LDS (.group_segment_fixed_size <= 160 KiB);
+  * reach no s_endpgm with an LDS-DMA of its own still in flight (in code order since the last vmcnt wait): a
+    workgroup that ends with pieces outstanding frees its LDS to the next workgroup while they land (VERDICT r4
+    #6, e.g. a persistent block's prefetch past its last tile).
 
 Usage: python tools/isa_audit.py [libdbsr_hip.so]   (prints one line per LDS-DMA kernel; exit 1 on a violation)
 Also imported by tests/test_capi.py."""
@@ -118,7 +121,7 @@ def audit(so_path):
                 # operations among the N youngest): a barrier that lets a wave pass with its LDS-DMAs in flight lets
                 # other waves read LDS that has not landed
                 ring = any(r in k for r in RING_KERNELS)
-                drain_ok, outstanding, waited = True, [], True
+                drain_ok, end_ok, outstanding, waited = True, True, [], True
                 for t in ins:
                     if re.match(r'^(buffer|global|flat)_(load|store|atomic)', t):
                         outstanding.append(bool(DMA_RE.search(t)))
@@ -133,14 +136,17 @@ def audit(so_path):
                         if (not waited) if ring else any(outstanding):
                             drain_ok = False
                         outstanding = []
+                    elif t.startswith('s_endpgm'):
+                        if any(outstanding) or not waited:
+                            end_ok = False
                 wg = md.get('wg_max', 256)
                 waves_per_simd_min = max(1, (wg // 64 + 3) // 4)
                 owns = regs * waves_per_simd_min >= 512 or regs >= 256 or ring
                 fits = md.get('lds', 0) <= 160 * 1024
                 declared = hi_v < regs and (hi_a == 0 or hi_a < md.get('agpr', 0))
-                ok = owns and m0_ok and fits and declared and drain_ok
+                ok = owns and m0_ok and fits and declared and drain_ok and end_ok
                 rows.append((k, len(dma), regs, hi_v, hi_a, md.get('lds', 0), wg, owns, m0_ok, declared, fits,
-                             drain_ok))
+                             drain_ok, end_ok))
                 if not ok:
                     bad.append(k)
     return rows, bad
@@ -150,9 +156,9 @@ def main():
     so = sys.argv[1] if len(sys.argv) > 1 else os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                              'deep-rawburst-sr_amd', 'libdbsr_hip.so')
     rows, bad = audit(so)
-    for k, n, regs, hv, ha, lds, wg, owns, m0, dec, fits, drain in rows:
-        print('%-90s dma %3d regs %3d (max v%d a%d) lds %6d wg %3d owns %d m0 %d declared %d lds-ok %d drain %d' % (
-            k[:90], n, regs, hv, ha, lds, wg, owns, m0, dec, fits, drain))
+    for k, n, regs, hv, ha, lds, wg, owns, m0, dec, fits, drain, end in rows:
+        print('%-90s dma %3d regs %3d (max v%d a%d) lds %6d wg %3d owns %d m0 %d declared %d lds-ok %d drain %d '
+              'end %d' % (k[:90], n, regs, hv, ha, lds, wg, owns, m0, dec, fits, drain, end))
     print('%d LDS-DMA kernels, %d violations' % (len(rows), len(bad)))
     sys.exit(1 if bad else 0)
 
