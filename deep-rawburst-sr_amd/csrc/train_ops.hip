@@ -94,8 +94,6 @@ __global__ __launch_bounds__(K == 3 ? 576 : 256) void conv_wgrad_kernel(
     for (int i = 0; i < NB; ++i)
 #pragma unroll
         for (int j = 0; j < NB; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    // 16-channel MFMA blocks that hold any of cout / cin (block-uniform: the rest multiply zeros)
-    const int ni = min(NB, (cout - co0 + 15) / 16), nj = min(NB, (cin - ci0 + 15) / 16);
     constexpr int EPP = 16 / (int)sizeof(T);           // elements per 16-B piece
     constexpr int PPR = CB / EPP;                      // pieces per CB-channel row
     constexpr int PIECES = (WG_PX + XPX) * PPR;
@@ -156,10 +154,9 @@ __global__ __launch_bounds__(K == 3 ? 576 : 256) void conv_wgrad_kernel(
             }
         }
     };
-    // full: every 16-channel block of the slice holds channels, so the MFMAs issue back to back (the
-    // per-block skip of a partial slice otherwise branches around each MFMA)
-    auto compute = [&](auto full) {
-        constexpr bool FULL = decltype(full)::value;
+    // every 16-channel block of the slice is computed (blocks past cout / cin multiply the zeros the staging
+    // loads there), so the MFMAs issue back to back
+    auto compute = [&]() {
         // ---- MFMAs ---- (k-steps not unrolled: one k-step's fragments live at a time)
 #pragma unroll 1
         for (int s = 0; s < 4; ++s) {
@@ -190,7 +187,7 @@ __global__ __launch_bounds__(K == 3 ? 576 : 256) void conv_wgrad_kernel(
                 for (int i = 0; i < NB; ++i)
 #pragma unroll
                     for (int j = 0; j < NB; ++j)
-                        if (FULL || (i < ni && j < nj)) acc[i][j] = mma16<T>(a[i], b[j], acc[i][j]);
+                        acc[i][j] = mma16<T>(a[i], b[j], acc[i][j]);
             } else {
                 // fp32: 8 MFMAs of k = 4 pixels; lane (kq = lane>>4, m = lane&15)
                 const int kq = lane >> 4, m = lane & 15;
@@ -218,20 +215,17 @@ __global__ __launch_bounds__(K == 3 ? 576 : 256) void conv_wgrad_kernel(
 #pragma unroll
     for (int d = 0; d < DIST; ++d)
         if (u0 + d < u1) fetch(u0 + d, pre[d]);
-    auto run = [&](auto full) {
-        for (long long u = u0; u < u1; u += DIST) {
+    for (long long u = u0; u < u1; u += DIST) {
 #pragma unroll
-            for (int d = 0; d < DIST; ++d) {
-                if (u + d >= u1) break;
-                put(pre[d]);
-                __syncthreads();
-                if (u + d + DIST < u1) fetch(u + d + DIST, pre[d]);
-                compute(full);
-                __syncthreads();
-            }
+        for (int d = 0; d < DIST; ++d) {
+            if (u + d >= u1) break;
+            put(pre[d]);
+            __syncthreads();
+            if (u + d + DIST < u1) fetch(u + d + DIST, pre[d]);
+            compute();
+            __syncthreads();
         }
-    };
-    run(std::true_type{});
+    }
     if (do_bias) {
         // the loop's last barrier has freed the LDS: thread t's EPP sums of channel group t % PPR, then channel c
         // adds the threads of its group in thread order
@@ -314,10 +308,10 @@ __global__ __launch_bounds__(K == 3 ? 576 : 256) void conv_wgrad_dma_kernel(
     const int ky = K == 3 ? wave / 3 : 0, kx = K == 3 ? wave % 3 : 0;
     const bool do_bias = bpart != nullptr && blockIdx.z == 0;          // block-uniform
     const bool bias_wave = do_bias && (K == 1 || wave == 5);
-    const int ni = min(NB, (cout - co0 + 15) / 16), nj = min(NB, (cin - ci0 + 15) / 16);
 
     // the lane's chunk of each of its pieces, relative to the tile, packed: pixel (ry + 2, rx + 2) and the
-    // channel offset; rows past the X tile get ry + 2 = 0xff (never in frame)
+    // channel offset; a chunk of the pitch padding / past the X tile gets the channel field 0xff, which no
+    // 16-bit slice reaches (CB <= 64 channels per block: c < 64), so its DMA always lands zeros
     int p_geo[C::PER];
 #pragma unroll
     for (int it = 0; it < C::PER; ++it) {
@@ -329,7 +323,7 @@ __global__ __launch_bounds__(K == 3 ? 576 : 256) void conv_wgrad_dma_kernel(
         } else {
             const int xr = row - WG_PX, o = K == 3 ? 1 : 0;
             ry = xr / C::XP - o; rx = xr % C::XP - o; c = (cp ^ wgd_swz<CB>(xr)) * 8;
-            if (xr >= C::XROWS || rx >= (K == 3 ? WG_HW - 1 : WG_TW)) ry = 0xff - 2;   // pitch padding / past the tile
+            if (xr >= C::XROWS || rx >= (K == 3 ? WG_HW - 1 : WG_TW)) c = 0xff;   // pitch padding / past the tile
         }
         p_geo[it] = ((ry + 2) << 16) | ((rx + 2) << 8) | c;
     }
@@ -351,7 +345,8 @@ __global__ __launch_bounds__(K == 3 ? 576 : 256) void conv_wgrad_dma_kernel(
             const int geo = p_geo[it];
             const int yy = y0 + (geo >> 16), xx = x0 + ((geo >> 8) & 0xff);
             const int c = (isdy ? co0 : ci0) + (geo & 0xff);
-            const bool ok = (unsigned)yy < (unsigned)h && (unsigned)xx < (unsigned)w && c < (isdy ? cout : cin);
+            const bool ok = (geo & 0xff) != 0xff && (unsigned)yy < (unsigned)h && (unsigned)xx < (unsigned)w &&
+                            c < (isdy ? cout : cin);
             const int off = ok ? ((yy * w + xx) * (isdy ? dy.ld : x.ld) + c) * 2 : BUF_OOB;
             wgd_dma(isdy ? (const void*)dyf : (const void*)xf, isdy ? dy_bytes : x_bytes, off,
                     lds0 + (unsigned)((stage * C::STAGE_U4 + piece * 64) * 16));
@@ -381,10 +376,9 @@ __global__ __launch_bounds__(K == 3 ? 576 : 256) void conv_wgrad_dma_kernel(
         for (int hf = 0; hf < 2; ++hf)
             offb[hf][i] = WG_PX * RB + (br0 + 4 * hf) * RB + ((cl ^ wgd_swz<CB>(br0 + 4 * hf)) << 4) + 8 * (p & 1);
     }
-    // full: every 16-channel block of the slice holds channels (cout, cin multiples of CB), so the MFMAs issue
-    // back to back; otherwise blocks past cout / cin are skipped (they would multiply zeros)
-    auto compute = [&](const unsigned char* st, auto full) {
-        constexpr bool FULL = decltype(full)::value;
+    // every 16-channel block of the slice is computed (blocks past cout / cin multiply the zeros their DMAs
+    // land), so the MFMAs issue back to back
+    auto compute = [&](const unsigned char* st) {
         // k-steps not unrolled: the fragments of one k-step live at a time (three waves per SIMD interleave)
 #pragma unroll 1
         for (int s = 0; s < 4; ++s) {
@@ -407,7 +401,7 @@ __global__ __launch_bounds__(K == 3 ? 576 : 256) void conv_wgrad_dma_kernel(
             for (int i = 0; i < NB; ++i)
 #pragma unroll
                 for (int j = 0; j < NB; ++j)
-                    if (FULL || (i < ni && j < nj)) acc[i][j] = mma16<T>(a[i], b[j], acc[i][j]);
+                    acc[i][j] = mma16<T>(a[i], b[j], acc[i][j]);
             if (bias_wave) {
 #pragma unroll
                 for (int i = 0; i < NB; ++i) {
@@ -426,17 +420,14 @@ __global__ __launch_bounds__(K == 3 ? 576 : 256) void conv_wgrad_dma_kernel(
     const long long nt = u1 - u0;
     if (nt > 0) issue(u0, 0);
     if (nt > 1) issue(u0 + 1, 1);
-    auto run = [&](auto full) {
-        for (long long t = 0; t < nt; ++t) {
-            // this wave's pieces of tile t landed (tile t + 1's, issued after them, may still be in flight) ...
-            if (t + 1 < nt) DBSR_VM_WAIT(C::PER);
-            else DBSR_VM_WAIT(0);
-            __syncthreads();            // ... and everyone's; every wave is done with tile t - 1's stage
-            if (t + 2 < nt) issue(u0 + t + 2, (int)((t + 2) % 3));
-            compute((const unsigned char*)(lds + (int)(t % 3) * C::STAGE_U4), full);
-        }
-    };
-    run(std::true_type{});
+    for (long long t = 0; t < nt; ++t) {
+        // this wave's pieces of tile t landed (tile t + 1's, issued after them, may still be in flight) ...
+        if (t + 1 < nt) DBSR_VM_WAIT(C::PER);
+        else DBSR_VM_WAIT(0);
+        __syncthreads();                // ... and everyone's; every wave is done with tile t - 1's stage
+        if (t + 2 < nt) issue(u0 + t + 2, (int)((t + 2) % 3));
+        compute((const unsigned char*)(lds + (int)(t % 3) * C::STAGE_U4));
+    }
     float* out = partial + ((long long)blockIdx.x * gridDim.y * gridDim.z + blockIdx.y * gridDim.z + blockIdx.z) *
                                (NW * CB * CB) + wave * CB * CB;
 #pragma unroll

@@ -175,6 +175,11 @@ class DBSRTrainer:
         self.blur = gauss_kernel3(up.gauss_blur_sd, up.gauss_ksz) if up.gauss_blur_sd is not None else None
         self.dec_post = [(T(b.conv1[0]), T(b.conv2[0])) for b in dec.post_res_layers]
         self.pred = T(dec.predictor[0])
+        if self.pred.cin != 32:
+            # the predictor's forward / backward (dbsr_head_forward / dbsr_head_backward) take 32 input channels,
+            # the reference's default dec_post_conv_dim: refuse here, not at the first step
+            raise NotImplementedError('DBSRTrainer: dec_post_conv_dim = %d; the HIP predictor head trains 32 '
+                                      'channels (dbsrnet_cvpr2021 default)' % self.pred.cin)
         # dgrad of the weight predictor's first conv, split: [base | diff] (ungated, to merge-prep) and the
         # offset features (gated by the offset-feature extractor's ReLU output)
         pd = self.proj.cout
