@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get('DBSR_HIP_LIB', os.path.join(_HERE, 'libdbsr_hip.so'))
 DBSR_F32, DBSR_BF16, DBSR_F16 = 0, 1, 2
 ACT_NONE, ACT_RELU, ACT_LRELU = 0, 1, 2
 OUT_NHWC, OUT_SHUFFLE, OUT_NCHW_F32 = 0, 1, 2
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 
 class FrameMap(ctypes.Structure):
@@ -90,6 +90,8 @@ def lib():
             'dbsr_conv_shuffle_blur_ok': ([ctypes.POINTER(ConvDesc)], c_int),
             'dbsr_resblock': ([ctypes.POINTER(ConvDesc), ctypes.POINTER(ConvDesc), c_void_p], c_int),
             'dbsr_resblock_ok': ([ctypes.POINTER(ConvDesc), ctypes.POINTER(ConvDesc)], c_int),
+            'dbsr_resblock_head': ([ctypes.POINTER(ConvDesc), ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_int, Tensor,
+                                    c_void_p], c_int),
             'dbsr_correlation': ([c_int, c_int, c_int, c_int, Tensor, Tensor, Tensor, c_int, c_void_p], c_int),
             'dbsr_correlation_backward': ([c_int, c_int, c_int, c_int, Tensor, Tensor, Tensor, Tensor, c_int, Tensor,
                                            Tensor, c_void_p], c_int),
@@ -167,7 +169,7 @@ def lib():
 
 EXPORTED = ['dbsr_abi_version', 'dbsr_last_error', 'dbsr_conv_packed_elems', 'dbsr_conv_pack_weights', 'dbsr_conv2d',
             'dbsr_set_conv_algo', 'dbsr_conv_kernel_for', 'dbsr_conv_dispatch_variant', 'dbsr_conv_lane_reach', 'dbsr_conv_workspace_bytes', 'dbsr_conv2d_head',
-            'dbsr_conv_head_ok', 'dbsr_conv_shuffle_blur', 'dbsr_conv_shuffle_blur_ok', 'dbsr_resblock', 'dbsr_resblock_ok',
+            'dbsr_conv_head_ok', 'dbsr_conv_shuffle_blur', 'dbsr_conv_shuffle_blur_ok', 'dbsr_resblock', 'dbsr_resblock_ok', 'dbsr_resblock_head',
             'dbsr_correlation', 'dbsr_correlation_backward', 'dbsr_backwarp', 'dbsr_warp_bilinear', 'dbsr_fuse_softmax',
             'dbsr_fuse_partial', 'dbsr_fuse_combine', 'dbsr_conv_fuse_softmax', 'dbsr_conv_fuse_ok',
             'dbsr_conv_transpose_k4s2', 'dbsr_pack_burst', 'dbsr_flow_finalize', 'dbsr_gauss_blur3',

@@ -1720,14 +1720,18 @@ __host__ __device__ __forceinline__ int rb_tile(int i, int b, int nb, int ntiles
     return i * nb + b;
 }
 
-template <typename T>
+// HEAD: the decoder's RGB predictor (decoders.py:61, 1x1 32 -> head_cout + ReLU) on the block's fp32 output, as
+// the pipelined kernel's epilogue 4 computes it (same products, order and lane reduction); k2.y is then the
+// head's fp32 NCHW output and the block's own output is not stored
+template <typename T, bool HEAD>
 __global__ __launch_bounds__(512, 1) void resblock32_kernel(ConvK k1, ConvK k2, int tiles_x, int tiles_y,
                                                             int ntiles) {
     using namespace rbk;
     DBSR_OWN_SIMDS();
-    __shared__ __attribute__((aligned(16))) u32x4_t lds[2 * IN_U4 + MID_U4 + 16];
+    __shared__ __attribute__((aligned(16))) u32x4_t lds[2 * IN_U4 + MID_U4 + 16 + 34];
     u32x4_t* lmid = lds + 2 * IN_U4;
     float* lbias = (float*)(lds + 2 * IN_U4 + MID_U4);            // [b1 (32)][b2 (32)]
+    float* lhead = lbias + 64;                                    // HEAD: weights [4][32], bias [4]
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int H = k1.in_h, W = k1.in_w;
 
@@ -1744,6 +1748,11 @@ __global__ __launch_bounds__(512, 1) void resblock32_kernel(ConvK k1, ConvK k2, 
         const ConvK& kb = threadIdx.x < 32 ? k1 : k2;
         lbias[threadIdx.x] = kb.bias ? kb.bias[threadIdx.x & 31] : 0.f;
     }
+    if constexpr (HEAD) {
+        if (threadIdx.x < 128) lhead[threadIdx.x] = (int)threadIdx.x < k2.head_cout * 32 ? k2.head_w[threadIdx.x] : 0.f;
+        if (threadIdx.x < 4)
+            lhead[128 + threadIdx.x] = (k2.head_b && (int)threadIdx.x < k2.head_cout) ? k2.head_b[threadIdx.x] : 0.f;
+    }
 
     struct Tile { const T* xf; long long y_off; int y0, x0; };
     auto decode = [&](int i) {
@@ -1752,7 +1761,8 @@ __global__ __launch_bounds__(512, 1) void resblock32_kernel(ConvK k1, ConvK k2, 
         const int tx = t % tiles_x, r = t / tiles_x, ty = r % tiles_y, f = r / tiles_y;
         tl.y0 = ty * TH; tl.x0 = tx * TW;
         tl.xf = (const T*)k1.x + map_frame(k1.xm, f) * k1.x_is;
-        tl.y_off = map_frame(k2.ym, f) * k2.y_is + k2.y_c0 + ((long long)tl.y0 * W + tl.x0) * k2.y_ld;
+        tl.y_off = HEAD ? map_frame(k2.ym, f) * k2.y_is + (long long)tl.y0 * W + tl.x0
+                        : map_frame(k2.ym, f) * k2.y_is + k2.y_c0 + ((long long)tl.y0 * W + tl.x0) * k2.y_ld;
         return tl;
     };
     const int my_tiles = ntiles / (int)gridDim.x + ((int)blockIdx.x < ntiles % (int)gridDim.x ? 1 : 0);
@@ -1813,6 +1823,16 @@ __global__ __launch_bounds__(512, 1) void resblock32_kernel(ConvK k1, ConvK k2, 
         __builtin_amdgcn_iglp_opt(0);
     };
 
+    // a conv2 group's output: 8 channels of a pixel (16-bit NHWC), or with HEAD lane g's head channel (fp32 NCHW)
+    auto store_out = [&](const Tile& tl, int i, int g, int col, const u32x4_t& o) {
+        const int q = wave + NW * i;
+        const long long px = (long long)(q >> 1) * W + 16 * (q & 1) + col;
+        if constexpr (HEAD) {
+            if (g < k2.head_cout) ((float*)k2.y)[tl.y_off + px + (long long)g * H * W] = __uint_as_float(o[0]);
+        } else {
+            *(u32x4_t*)((T*)k2.y + tl.y_off + px * k2.y_ld + 8 * g) = o;
+        }
+    };
     Tile cur = decode(0), prev = cur;
     if (my_tiles > 0) dma(cur, 0);
     u32x4_t outv[Q2];                   // the previous tile's conv2 outputs, stored after this tile's first barrier
@@ -1825,11 +1845,7 @@ __global__ __launch_bounds__(512, 1) void resblock32_kernel(ConvK k1, ConvK k2, 
         const int g = ln >> 4, col = ln & 15;
         if (ti > 0) {
 #pragma unroll
-            for (int i = 0; i < Q2; ++i) {
-                const int q = wave + NW * i;
-                *(u32x4_t*)((T*)k2.y + prev.y_off + ((long long)(q >> 1) * W + 16 * (q & 1) + col) * k2.y_ld + 8 * g) =
-                    outv[i];
-            }
+            for (int i = 0; i < Q2; ++i) store_out(prev, i, g, col, outv[i]);
         }
         const u32x4_t* lin = lds + (ti & 1) * IN_U4;
         const bool more = ti + 1 < my_tiles;
@@ -1897,9 +1913,34 @@ __global__ __launch_bounds__(512, 1) void resblock32_kernel(ConvK k1, ConvK k2, 
                         v[4 + r] = acc[j][1][r] + bv[4 + r];
                     }
                     u32x4_t o;
+                    if constexpr (HEAD) {
+                        // the pipelined kernel's epilogue 4: fp32 ReLU(v + residual), partial head sums over this
+                        // lane's 8 channels, reduced over the column's four g lanes; lane g keeps channel g
 #pragma unroll
-                    for (int e = 0; e < 4; ++e)
-                        o[e] = relu16x2(H16<T>::pack(v[2 * e] + H16<T>::lo(rq[e]), v[2 * e + 1] + H16<T>::hi(rq[e])));
+                        for (int e = 0; e < 4; ++e) {
+                            v[2 * e] = fmaxf(v[2 * e] + H16<T>::lo(rq[e]), 0.f);
+                            v[2 * e + 1] = fmaxf(v[2 * e + 1] + H16<T>::hi(rq[e]), 0.f);
+                        }
+                        float hs[4];
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) {
+                            const float4 w0 = *(const float4*)(lhead + c * 32 + 8 * g);
+                            const float4 w1 = *(const float4*)(lhead + c * 32 + 8 * g + 4);
+                            float a = v[0] * w0.x;
+                            a = fmaf(v[1], w0.y, a); a = fmaf(v[2], w0.z, a); a = fmaf(v[3], w0.w, a);
+                            a = fmaf(v[4], w1.x, a); a = fmaf(v[5], w1.y, a); a = fmaf(v[6], w1.z, a);
+                            a = fmaf(v[7], w1.w, a);
+                            a += __shfl_xor(a, 16, 64);
+                            a += __shfl_xor(a, 32, 64);
+                            hs[c] = a;
+                        }
+                        const float hv = g == 0 ? hs[0] : g == 1 ? hs[1] : g == 2 ? hs[2] : hs[3];
+                        o = u32x4_t{__float_as_uint(fmaxf(hv + lhead[128 + g], 0.f)), 0u, 0u, 0u};
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            o[e] = relu16x2(H16<T>::pack(v[2 * e] + H16<T>::lo(rq[e]), v[2 * e + 1] + H16<T>::hi(rq[e])));
+                    }
                     outv[NG * bt + j] = o;
                 }
             });
@@ -1908,12 +1949,8 @@ __global__ __launch_bounds__(512, 1) void resblock32_kernel(ConvK k1, ConvK k2, 
         cur = nxt;
     }
     if (my_tiles > 0) {
-        const int g = lane >> 4, col = lane & 15;
 #pragma unroll
-        for (int i = 0; i < Q2; ++i) {
-            const int q = wave + NW * i;
-            *(u32x4_t*)((T*)k2.y + prev.y_off + ((long long)(q >> 1) * W + 16 * (q & 1) + col) * k2.y_ld + 8 * g) = outv[i];
-        }
+        for (int i = 0; i < Q2; ++i) store_out(prev, i, lane >> 4, lane & 15, outv[i]);
     }
     vm_drain();                         // (no LDS-DMA outstanding at s_endpgm: tools/isa_audit.py)
 }
@@ -2888,24 +2925,51 @@ extern "C" int dbsr_resblock_ok(const dbsr_conv_desc* c1, const dbsr_conv_desc* 
     return use_resblock32(c1, c2) ? 1 : 0;
 }
 
-extern "C" int dbsr_resblock(const dbsr_conv_desc* c1, const dbsr_conv_desc* c2, void* stream) {
-    DBSR_CHECK_ARG(c1 && c2 && c1->x.ptr && c1->w && c2->w && c2->y.ptr, "resblock: null pointer");
+int resblock_launch(const dbsr_conv_desc* c1, const dbsr_conv_desc* c2, const float* head_w, const float* head_b,
+                    int head_cout, const dbsr_tensor* head_out, void* stream) {
+    DBSR_CHECK_ARG(c1 && c2 && c1->x.ptr && c1->w && c2->w, "resblock: null pointer");
+    DBSR_CHECK_ARG(head_out || c2->y.ptr, "resblock: null output");
     DBSR_CHECK_ARG(c1->x.map.fpg > 0 && c2->y.map.fpg > 0 && c1->n_frames > 0, "resblock: bad frame map / sizes");
     DBSR_CHECK_ARG(use_resblock32(c1, c2), "resblock: needs two 16-bit 3x3/s1/p1 32 -> 32 convs (conv1 ReLU; conv2 "
                    "residual = conv1's input, post-ReLU), frames a multiple of 32 x 16, NHWC slices aligned to 8");
-    const ConvK k1 = make_convk(c1), k2 = make_convk(c2);
+    const ConvK k1 = make_convk(c1);
+    ConvK k2 = make_convk(c2);
+    if (head_out) {
+        DBSR_CHECK_ARG(head_w && head_out->ptr, "resblock_head: null pointer");
+        DBSR_CHECK_ARG(head_cout >= 1 && head_cout <= 4, "resblock_head: head_cout must be 1..4");
+        DBSR_CHECK_ARG(head_out->dtype == DBSR_F32 && head_out->map.fpg > 0, "resblock_head: fp32 NCHW output");
+        k2.head_w = head_w; k2.head_b = head_b; k2.head_cout = head_cout;
+        k2.y = head_out->ptr; k2.y_f32 = 1; k2.y_is = head_out->img_stride; k2.y_ld = 1; k2.y_c0 = 0;
+        k2.ym = head_out->map;
+    }
     const int tiles_x = c1->in_w / rbk::TW, tiles_y = c1->in_h / rbk::TH;
     const int ntiles = c1->n_frames * tiles_x * tiles_y;
     int grid = c1->max_blocks > 0 ? std::min(c1->max_blocks, num_cus()) : num_cus();
     grid = std::min(grid, ntiles);
     DBSR_CHECK_ARG(rb_mapping_ok(grid, ntiles), "resblock: tile mapping out of range (grid %d, %d tiles)", grid, ntiles);
     hipStream_t s = (hipStream_t)stream;
-    if (c1->x.dtype == DBSR_F16)
-        hipLaunchKernelGGL(resblock32_kernel<f16_t>, dim3(grid), dim3(512), 0, s, k1, k2, tiles_x, tiles_y, ntiles);
-    else
-        hipLaunchKernelGGL(resblock32_kernel<bf16_t>, dim3(grid), dim3(512), 0, s, k1, k2, tiles_x, tiles_y, ntiles);
+    if (k2.head_w) {
+        if (c1->x.dtype == DBSR_F16)
+            hipLaunchKernelGGL((resblock32_kernel<f16_t, true>), dim3(grid), dim3(512), 0, s, k1, k2, tiles_x, tiles_y, ntiles);
+        else
+            hipLaunchKernelGGL((resblock32_kernel<bf16_t, true>), dim3(grid), dim3(512), 0, s, k1, k2, tiles_x, tiles_y, ntiles);
+    } else {
+        if (c1->x.dtype == DBSR_F16)
+            hipLaunchKernelGGL((resblock32_kernel<f16_t, false>), dim3(grid), dim3(512), 0, s, k1, k2, tiles_x, tiles_y, ntiles);
+        else
+            hipLaunchKernelGGL((resblock32_kernel<bf16_t, false>), dim3(grid), dim3(512), 0, s, k1, k2, tiles_x, tiles_y, ntiles);
+    }
     DBSR_LAUNCH_CHECK();
     return 0;
+}
+
+extern "C" int dbsr_resblock(const dbsr_conv_desc* c1, const dbsr_conv_desc* c2, void* stream) {
+    return resblock_launch(c1, c2, nullptr, nullptr, 0, nullptr, stream);
+}
+
+extern "C" int dbsr_resblock_head(const dbsr_conv_desc* c1, const dbsr_conv_desc* c2, const float* head_w,
+                                  const float* head_b, int head_cout, dbsr_tensor head_out, void* stream) {
+    return resblock_launch(c1, c2, head_w, head_b, head_cout, &head_out, stream);
 }
 
 extern "C" int dbsr_conv_shuffle_blur_ok(const dbsr_conv_desc* d) { return use_upsample_blur(d) ? 1 : 0; }

@@ -283,9 +283,11 @@ class Plan:
         self.kernel[len(self.ops) - 1] = 'conv_fuse'
         return len(self.ops) - 1
 
-    def resblock(self, name, c1, c2, n_frames, x, mid, y, hw):
+    def resblock(self, name, c1, c2, n_frames, x, mid, y, hw, head=None):
         """ResBlock (blocks.py:81-96) x -> y as one launch (dbsr_resblock: the intermediate stays in the LDS) when
-        the library serves it; returns False otherwise (the caller then emits conv1 into `mid` and conv2)."""
+        the library serves it; returns False otherwise (the caller then emits conv1 into `mid` and conv2).
+        head = (name, w [hc, 32] fp32, b | None, out_desc): the RGB predictor fused as well (dbsr_resblock_head;
+        y is then not written)."""
         d1 = self._desc(name + '.conv1', c1, n_frames, x, 0, hw, mid, 0, L.ACT_RELU, IDENTITY, IDENTITY, None, 0,
                         IDENTITY, L.ACT_NONE, L.OUT_NHWC, 0, None, None, False, None, 0, IDENTITY)
         d2 = self._desc(name + '.conv2', c2, n_frames, mid, 0, hw, y, 0, L.ACT_NONE, IDENTITY, IDENTITY, x, 0,
@@ -295,7 +297,15 @@ class Plan:
         self.convs.extend([(d1, self.lane), (d2, self.lane)])
         oh, ow = d1.out_h, d1.out_w
         flop = 2.0 * n_frames * oh * ow * (c1.cout * d1.cin * 9 + c2.cout * d2.cin * 9)
-        self.add(name, L.lib().dbsr_resblock, ctypes.byref(d1), ctypes.byref(d2), work=('flop', flop))
+        if head is not None:
+            hname, hw_, hb, hdesc = head
+            self.keep.extend([hw_, hb, hdesc])
+            flop += 2.0 * n_frames * oh * ow * hw_.shape[0] * hw_.shape[1]
+            self.add(name + '+' + hname, L.lib().dbsr_resblock_head, ctypes.byref(d1), ctypes.byref(d2),
+                     hw_.data_ptr(), hb.data_ptr() if hb is not None else None, hw_.shape[0], hdesc,
+                     work=('flop', flop))
+        else:
+            self.add(name, L.lib().dbsr_resblock, ctypes.byref(d1), ctypes.byref(d2), work=('flop', flop))
         self.kernel[len(self.ops) - 1] = 'resblock32'
         return True
 
@@ -748,9 +758,10 @@ class DBSREngine:
         fused = False
         for i, (c1, c2) in enumerate(blocks):
             b, c = [j for j in range(3) if j != a]
-            last_head = head is not None and i == len(blocks) - 1
-            if DBSREngine.FUSED_RESBLOCK and not last_head and \
-                    plan.resblock(f'{name}{i}', c1, c2, n, bufs[a], bufs[b], bufs[c], hw):
+            hd = head if head is not None and i == len(blocks) - 1 else None
+            if DBSREngine.FUSED_RESBLOCK and \
+                    plan.resblock(f'{name}{i}', c1, c2, n, bufs[a], bufs[b], bufs[c], hw, head=hd):
+                fused = hd is not None
                 a = c
                 continue
             plan.conv(f'{name}{i}.conv1', c1, n, bufs[a], 0, hw, bufs[b], 0, L.ACT_RELU)

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define DBSR_ABI_VERSION 17
+#define DBSR_ABI_VERSION 18
 
 enum { DBSR_F32 = 0, DBSR_BF16 = 1, DBSR_F16 = 2 };
 enum { DBSR_ACT_NONE = 0, DBSR_ACT_RELU = 1, DBSR_ACT_LRELU = 2 };      /* LeakyReLU slope 0.1 */
@@ -157,6 +157,12 @@ int dbsr_conv_shuffle_blur_ok(const dbsr_conv_desc* d);
  * NHWC slices aligned to 8 channels; c1->max_blocks caps the persistent grid. */
 int dbsr_resblock(const dbsr_conv_desc* c1, const dbsr_conv_desc* c2, void* stream);
 int dbsr_resblock_ok(const dbsr_conv_desc* c1, const dbsr_conv_desc* c2);
+/* dbsr_resblock with the decoder's RGB predictor fused (ABI 18; decoders.py:59-61, the last post-ResBlock + the
+ * 1x1 32 -> head_cout conv + ReLU, as dbsr_conv2d_head computes it): the block's fp32 output stays in registers
+ * and out = ReLU(head_w . t + head_b) is stored fp32 NCHW (head_out.img_stride = head_cout*h*w); c2->y is not
+ * written.  head_w fp32 [head_cout][32], head_b [head_cout] or NULL, head_cout 1..4; requires dbsr_resblock_ok. */
+int dbsr_resblock_head(const dbsr_conv_desc* c1, const dbsr_conv_desc* c2, const float* head_w, const float* head_b,
+                       int head_cout, dbsr_tensor head_out, void* stream);
 /* 1 when dbsr_conv2d_head accepts `d`: pipelined shape (bf16 3x3/s1/p1, width % 64 == 0, height % 8 == 0,
  * >= 256 tiles), cout == 32, residual, act none, post-act ReLU. */
 int dbsr_conv_head_ok(const dbsr_conv_desc* d);
