@@ -164,21 +164,34 @@ inline bool blur_separable(const float* k9, Blur3& b) {
         }
     return true;
 }
-// horizontal pass over one row of 8 channels: x0, x1, x2 = columns -1, 0, +1 (16-bit, raw)
+// horizontal pass over one row of 8 channels: x0, x1, x2 = columns -1, 0, +1 (16-bit, raw).  Channel pairs run as
+// packed fp32 ops (v_pk_mul_f32 / v_pk_fma_f32: each component is the scalar mul / fma, so the sums are bitwise the
+// scalar ones) -- half the VALU issue of the blur, which bounds the fused upsampler
 template <typename T>
 __device__ __forceinline__ void blur_row(const Blur3& b, const u32x4_t& x0, const u32x4_t& x1, const u32x4_t& x2,
                                          float (&h)[8]) {
+    const f32x2_t k0 = {b.kh[0], b.kh[0]}, k1 = {b.kh[1], b.kh[1]}, k2 = {b.kh[2], b.kh[2]};
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        h[2 * q] = fmaf(b.kh[2], H16<T>::lo(x2[q]), fmaf(b.kh[1], H16<T>::lo(x1[q]), b.kh[0] * H16<T>::lo(x0[q])));
-        h[2 * q + 1] = fmaf(b.kh[2], H16<T>::hi(x2[q]), fmaf(b.kh[1], H16<T>::hi(x1[q]), b.kh[0] * H16<T>::hi(x0[q])));
+        const f32x2_t v0 = {H16<T>::lo(x0[q]), H16<T>::hi(x0[q])};
+        const f32x2_t v1 = {H16<T>::lo(x1[q]), H16<T>::hi(x1[q])};
+        const f32x2_t v2 = {H16<T>::lo(x2[q]), H16<T>::hi(x2[q])};
+        const f32x2_t r = __builtin_elementwise_fma(k2, v2, __builtin_elementwise_fma(k1, v1, k0 * v0));
+        h[2 * q] = r.x;
+        h[2 * q + 1] = r.y;
     }
 }
 // vertical pass: rows -1, 0, +1 of horizontal sums
 __device__ __forceinline__ void blur_col(const Blur3& b, const float (&h0)[8], const float (&h1)[8], const float (&h2)[8],
                                          float (&o)[8]) {
+    const f32x2_t k0 = {b.kv[0], b.kv[0]}, k1 = {b.kv[1], b.kv[1]}, k2 = {b.kv[2], b.kv[2]};
 #pragma unroll
-    for (int q = 0; q < 8; ++q) o[q] = fmaf(b.kv[2], h2[q], fmaf(b.kv[1], h1[q], b.kv[0] * h0[q]));
+    for (int q = 0; q < 4; ++q) {
+        const f32x2_t a0 = {h0[2 * q], h0[2 * q + 1]}, a1 = {h1[2 * q], h1[2 * q + 1]}, a2 = {h2[2 * q], h2[2 * q + 1]};
+        const f32x2_t r = __builtin_elementwise_fma(k2, a2, __builtin_elementwise_fma(k1, a1, k0 * a0));
+        o[2 * q] = r.x;
+        o[2 * q + 1] = r.y;
+    }
 }
 
 // compile-time loop: f(std::integral_constant<int, I>) for I in [I0, I1) (register arrays indexed by I stay

@@ -1789,14 +1789,15 @@ __global__ __launch_bounds__(512, 1) void resblock32_kernel(ConvK k1, ConvK k2, 
 
     // the 9 taps of NG 16-pixel groups (image rows iw wide, group j's tap-(0,0) pixel P0[j]): B-fragments read
     // two taps ahead (a 3-deep ring per group)
-    auto taps = [&](const u32x4_t* img, int iw, int g, const int (&P0)[NG], const Frag<T> (&w)[9][2],
-                    f32x4_t (&acc)[NG][2]) {
-        int bs[NG][8];
+    // (NB = the batch's group count: NG, or the lone last group of conv1's odd count)
+    auto taps = [&](const u32x4_t* img, int iw, int g, const auto& P0, const Frag<T> (&w)[9][2], auto& acc) {
+        constexpr int NB = std::extent<std::remove_reference_t<decltype(P0)>>::value;
+        int bs[NB][8];
 #pragma unroll
-        for (int j = 0; j < NG; ++j)
+        for (int j = 0; j < NB; ++j)
 #pragma unroll
             for (int rho = 0; rho < 8; ++rho) bs[j][rho] = 4 * P0[j] + halo_phys(P0[j] + rho, g);
-        Frag<T> bq[NG][3];
+        Frag<T> bq[NB][3];
         auto rd = [&](int j, int tap) {
             const int imm = (tap / 3) * iw + tap % 3;
             Frag<T> b;
@@ -1804,7 +1805,7 @@ __global__ __launch_bounds__(512, 1) void resblock32_kernel(ConvK k1, ConvK k2, 
             return b;
         };
 #pragma unroll
-        for (int j = 0; j < NG; ++j) {
+        for (int j = 0; j < NB; ++j) {
             bq[j][0] = rd(j, 0);
             bq[j][1] = rd(j, 1);
         }
@@ -1812,7 +1813,7 @@ __global__ __launch_bounds__(512, 1) void resblock32_kernel(ConvK k1, ConvK k2, 
             constexpr int tap = decltype(t_)::value;
             const f32x4_t z = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int j = 0; j < NG; ++j) {
+            for (int j = 0; j < NB; ++j) {
                 acc[j][0] = mma(w[tap][0], bq[j][tap % 3], tap == 0 ? z : acc[j][0]);
                 acc[j][1] = mma(w[tap][1], bq[j][tap % 3], tap == 0 ? z : acc[j][1]);
                 if constexpr (tap + 2 < 9) bq[j][(tap + 2) % 3] = rd(j, tap + 2);
@@ -1851,24 +1852,25 @@ __global__ __launch_bounds__(512, 1) void resblock32_kernel(ConvK k1, ConvK k2, 
         const bool more = ti + 1 < my_tiles;
         const Tile nxt = more ? decode(ti + 1) : cur;
         if (more) dma(nxt, (ti + 1) & 1);
-        // ---- conv1 on the intermediate region: groups wave + 4 i, in batches of NG ----
+        // ---- conv1 on the intermediate region: groups wave + 8 i, in batches of NG and a lone last group (the odd
+        // fifth: batching it with a clamped duplicate cost a sixth of conv1's MFMAs and LDS reads) ----
         {
             const float4 b0 = *(const float4*)(lbias + 8 * g), b1 = *(const float4*)(lbias + 8 * g + 4);
             const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-            StaticFor<0, (Q1 + NG - 1) / NG>::run([&](auto bt_) {
-                constexpr int bt = decltype(bt_)::value;
-                int pa[NG], P0[NG];
+            auto conv1 = [&](auto nb_, auto q0_) {
+                constexpr int NB = decltype(nb_)::value, Q0 = decltype(q0_)::value;
+                int pa[NB], P0[NB];
 #pragma unroll
-                for (int j = 0; j < NG; ++j) {
-                    pa[j] = min(16 * (wave + NW * (NG * bt + j)) + col, MPX - 1);
+                for (int j = 0; j < NB; ++j) {
+                    pa[j] = min(16 * (wave + NW * (Q0 + j)) + col, MPX - 1);
                     const int r = pa[j] / MW, c = pa[j] - r * MW;
                     P0[j] = r * IW + c;
                 }
-                f32x4_t acc[NG][2];
+                f32x4_t acc[NB][2];
                 taps(lin, IW, g, P0, w1, acc);
 #pragma unroll
-                for (int j = 0; j < NG; ++j) {
-                    const int p = 16 * (wave + NW * (NG * bt + j)) + col;
+                for (int j = 0; j < NB; ++j) {
+                    const int p = 16 * (wave + NW * (Q0 + j)) + col;
                     const int r = pa[j] / MW, c = pa[j] - r * MW;
                     const int fy = cur.y0 - 1 + r, fx = cur.x0 - 1 + c;
                     const bool inside = (unsigned)fy < (unsigned)H && (unsigned)fx < (unsigned)W;
@@ -1882,7 +1884,15 @@ __global__ __launch_bounds__(512, 1) void resblock32_kernel(ConvK k1, ConvK k2, 
                     if (!inside) o = u32x4_t{0u, 0u, 0u, 0u};
                     if (p < MPX) lmid[4 * p + halo_phys(p, g)] = o;
                 }
+            };
+            StaticFor<0, Q1 / NG>::run([&](auto bt_) {
+                conv1(std::integral_constant<int, NG>{}, std::integral_constant<int, NG * decltype(bt_)::value>{});
             });
+            if constexpr (Q1 % NG != 0) {
+                // wave-uniform: the waves whose last group lies inside the region (wave 7's fifth does not)
+                if (wave + NW * (Q1 - Q1 % NG) < G1)
+                    conv1(std::integral_constant<int, Q1 % NG>{}, std::integral_constant<int, Q1 - Q1 % NG>{});
+            }
         }
         dma_barrier();                  // B1: the intermediate image is complete (the next halo's DMA, issued before
                                         // conv1, has landed too: no LDS-DMA crosses a barrier in flight)
@@ -1967,6 +1977,34 @@ bool rb_mapping_ok(int nb, int ntiles) {
         }
     }
     return true;
+}
+
+// byte range [lo, hi) that `n` frames of t cover: each stored image from its first used element (c0) to the last
+// pixel's last element (per_img elements past the image base: NHWC (hw - 1) * ld + c0 + ch, NCHW its plane count)
+void tensor_span(const dbsr_tensor& t, int n, long long per_img, int es, unsigned long long& lo,
+                 unsigned long long& hi) {
+    long long mn = 0, mx = 0;
+    for (int f = 0; f < n; ++f) {
+        const long long img = (long long)(f / t.map.fpg) * t.map.group_stride + t.map.group_offset +
+                              (long long)(f % t.map.fpg) * t.map.inner_stride;
+        if (f == 0 || img < mn) mn = img;
+        if (f == 0 || img > mx) mx = img;
+    }
+    const unsigned long long base = (unsigned long long)(uintptr_t)t.ptr;
+    lo = base + (unsigned long long)((mn * t.img_stride + t.c0) * es);
+    hi = base + (unsigned long long)((mx * t.img_stride + per_img) * es);
+}
+// the persistent ResBlock kernel reads neighbouring tiles' input halos while other blocks store finished tiles, so
+// its output (c2->y, or the head's fp32 NCHW output) must not overlap its input x (an in-place call
+// y == x would race; the two-call path it replaces is in-place safe)
+bool resblock_out_disjoint(const dbsr_conv_desc* c1, const dbsr_conv_desc* c2, const dbsr_tensor* head_out,
+                           int head_cout) {
+    const long long hw = (long long)c1->in_h * c1->in_w;
+    unsigned long long xl, xh, yl, yh;
+    tensor_span(c1->x, c1->n_frames, (hw - 1) * c1->x.ld + c1->x.c0 + 32, 2, xl, xh);
+    if (head_out) tensor_span(*head_out, c1->n_frames, (long long)head_cout * hw, 4, yl, yh);
+    else tensor_span(c2->y, c1->n_frames, (hw - 1) * c2->y.ld + c2->y.c0 + 32, 2, yl, yh);
+    return yh <= xl || xh <= yl;
 }
 
 // the fused ResBlock applies: c1 = conv1 (x -> any, ReLU), c2 = conv2 (-> y, residual x, post-ReLU), both
@@ -2922,7 +2960,7 @@ extern "C" int dbsr_conv2d(const dbsr_conv_desc* d, void* stream) {
 }
 
 extern "C" int dbsr_resblock_ok(const dbsr_conv_desc* c1, const dbsr_conv_desc* c2) {
-    return use_resblock32(c1, c2) ? 1 : 0;
+    return use_resblock32(c1, c2) && c2->y.ptr && resblock_out_disjoint(c1, c2, nullptr, 0) ? 1 : 0;
 }
 
 int resblock_launch(const dbsr_conv_desc* c1, const dbsr_conv_desc* c2, const float* head_w, const float* head_b,
@@ -2942,6 +2980,8 @@ int resblock_launch(const dbsr_conv_desc* c1, const dbsr_conv_desc* c2, const fl
         k2.y = head_out->ptr; k2.y_f32 = 1; k2.y_is = head_out->img_stride; k2.y_ld = 1; k2.y_c0 = 0;
         k2.ym = head_out->map;
     }
+    DBSR_CHECK_ARG(resblock_out_disjoint(c1, c2, head_out, head_cout),
+                   "resblock: the output must not overlap the input x (other blocks still read x's halos)");
     const int tiles_x = c1->in_w / rbk::TW, tiles_y = c1->in_h / rbk::TH;
     const int ntiles = c1->n_frames * tiles_x * tiles_y;
     int grid = c1->max_blocks > 0 ? std::min(c1->max_blocks, num_cus()) : num_cus();

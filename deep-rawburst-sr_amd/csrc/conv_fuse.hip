@@ -507,7 +507,9 @@ extern "C" int dbsr_conv_fuse_softmax(const dbsr_conv_desc* d, int B, int N, dbs
     DBSR_CHECK_ARG(nt < (1LL << 31), "conv_fuse_softmax: grid too large");
     const int cap = d->max_blocks > 0 ? std::min(d->max_blocks, fuse_cus()) : fuse_cus();
     int grid = (int)std::min<long long>(nt, cap);
-    grid = (grid + 7) / 8 * 8;
+    // a multiple of 8 (the XCD-grouped walk), rounded DOWN so a max_blocks cap is not exceeded (each
+    // block takes ~160 KB of LDS and its SIMDs, CUs meant for a concurrent lane); at least 8 (surplus blocks exit)
+    grid = grid >= 8 ? grid / 8 * 8 : 8;
     hipStream_t s = (hipStream_t)stream;
     if (dt == DBSR_F16)
         hipLaunchKernelGGL((conv_fuse_kernel<f16_t, FUSE_NF>), dim3(grid), dim3(512), 0, s, k, tiles_x, tiles_y, nct,

@@ -191,6 +191,7 @@ class Plan:
         self.keep = []
         self.work = {}       # op index -> ('flop' | 'byte', algorithmic amount per launch)
         self.kernel = {}     # op index -> kernel family (convs)
+        self.hbm = {}        # op index -> algorithmic HBM bytes per launch of the fused conv kernels (bench.py)
         self.convs = []      # (ConvDesc, lane): each lane shares one split-K workspace
         self.lane = 0
         self.lanes = {0}
@@ -268,11 +269,11 @@ class Plan:
                                                                                       'conv2d_generic')
         return d
 
-    def conv_fuse(self, name, pc, B, N, x, in_hw, ref, oth, fused, weights):
+    def conv_fuse(self, name, pc, B, N, x, in_hw, ref, oth, fused, weights, xmap=IDENTITY):
         """The weight predictor's last conv + softmax over the burst + fusion in one launch
         (dbsr_conv_fuse_softmax: the logits never reach memory).  Returns the op index, or None when the
         library does not serve the shape (the caller then emits the conv and dbsr_fuse_softmax)."""
-        d = self._desc(name, pc, B * N, x, 0, in_hw, None, 0, L.ACT_NONE, IDENTITY, IDENTITY, None, 0, IDENTITY,
+        d = self._desc(name, pc, B * N, x, 0, in_hw, None, 0, L.ACT_NONE, xmap, IDENTITY, None, 0, IDENTITY,
                        L.ACT_NONE, L.OUT_NHWC, 0, L.NULL_TENSOR, None, False, None, 0, IDENTITY)
         if not L.lib().dbsr_conv_fuse_ok(ctypes.byref(d), B, N):
             return None
@@ -281,6 +282,9 @@ class Plan:
         self.add(name, L.lib().dbsr_conv_fuse_softmax, ctypes.byref(d), B, N, ref, oth, fused, weights,
                  work=('flop', flop))
         self.kernel[len(self.ops) - 1] = 'conv_fuse'
+        # hidden input + the N frames' features in + fusion weights out (when written) + fused out
+        es, C = (4 if x.dtype == torch.float32 else 2), pc.cout
+        self.hbm[len(self.ops) - 1] = es * B * H * W * (N * d.cin + N * C + (N * C if weights.ptr else 0) + C)
         return len(self.ops) - 1
 
     def resblock(self, name, c1, c2, n_frames, x, mid, y, hw, head=None):
@@ -307,6 +311,8 @@ class Plan:
         else:
             self.add(name, L.lib().dbsr_resblock, ctypes.byref(d1), ctypes.byref(d2), work=('flop', flop))
         self.kernel[len(self.ops) - 1] = 'resblock32'
+        # x in once; y out (16-bit, 32 ch) or the head's fp32 NCHW planes
+        self.hbm[len(self.ops) - 1] = n_frames * oh * ow * (2 * 32 + (4 * head[1].shape[0] if head is not None else 2 * 32))
         return True
 
     def conv_shuffle_blur(self, name, pc, n_frames, x, in_hw, y, act, k9):
@@ -323,6 +329,9 @@ class Plan:
         flop = 2.0 * n_frames * d.out_h * d.out_w * pc.cout * d.cin
         self.add(name, L.lib().dbsr_conv_shuffle_blur, ctypes.byref(d), kbuf, work=('flop', flop))
         self.kernel[len(self.ops) - 1] = 'conv1x1_shuffle_blur'
+        # low-res input in, the blurred high-res output out (16-bit)
+        s = pc.shuffle
+        self.hbm[len(self.ops) - 1] = 2 * n_frames * d.out_h * d.out_w * (d.cin + pc.cout // (s * s) * s * s)
         return d
 
     def _desc(self, name, pc, n_frames, x, xc0, in_hw, y, yc0, act, xmap, ymap, res, rc0, rmap, post_act, out_mode,
@@ -1017,8 +1026,9 @@ class DBSREngine:
         if pred_out is None:
             pred_out = bufs['pred'] = torch.zeros(B, 3, H * S, W * S, dtype=torch.float32, device=dev)
         pdesc = L.tensor_desc(pred_out, 1, 0, img_stride=3 * H * S * W * S, dtype=torch.float32)
-        # bf16: the last post ResBlock's conv2 and the RGB predictor in one kernel (its 32-channel output
-        # never reaches HBM; the head runs fp32 on the fp32 ResBlock output, decoders.py:59-61)
+        # 16-bit (fp16 / bf16): the last post ResBlock and the RGB predictor in one kernel -- dbsr_resblock_head where
+        # the fused ResBlock serves the shape, else the pipelined conv2's epilogue 4 (dbsr_conv2d_head); the block's
+        # 32-channel output never reaches HBM and the head runs fp32 on its unrounded value (decoders.py:59-61)
         head = None
         if dt != torch.float32 and self.dec_post and DBSREngine.FUSED_HEAD:
             head = ('predictor', self.head_w, self.head_b, pdesc)

@@ -154,7 +154,8 @@ int dbsr_conv_shuffle_blur_ok(const dbsr_conv_desc* d);
  * (x -> its y, act ReLU), c2 = conv2 (its x, y, residual = c1's input, act none, post-act ReLU); c1->y and c2->x
  * name the intermediate, which this call neither reads nor writes (it stays on chip).  Bitwise equal to the two
  * calls.  Requires dbsr_resblock_ok(c1, c2): 16-bit 3x3/s1/p1 convs 32 -> 32, frames a multiple of 32 x 16,
- * NHWC slices aligned to 8 channels; c1->max_blocks caps the persistent grid. */
+ * NHWC slices aligned to 8 channels, and y not overlapping x (blocks read neighbouring tiles' halos of x while
+ * others store y: an in-place call is refused with DBSR_E_ARG); c1->max_blocks caps the persistent grid. */
 int dbsr_resblock(const dbsr_conv_desc* c1, const dbsr_conv_desc* c2, void* stream);
 int dbsr_resblock_ok(const dbsr_conv_desc* c1, const dbsr_conv_desc* c2);
 /* dbsr_resblock with the decoder's RGB predictor fused (ABI 18; decoders.py:59-61, the last post-ResBlock + the
@@ -163,8 +164,9 @@ int dbsr_resblock_ok(const dbsr_conv_desc* c1, const dbsr_conv_desc* c2);
  * written.  head_w fp32 [head_cout][32], head_b [head_cout] or NULL, head_cout 1..4; requires dbsr_resblock_ok. */
 int dbsr_resblock_head(const dbsr_conv_desc* c1, const dbsr_conv_desc* c2, const float* head_w, const float* head_b,
                        int head_cout, dbsr_tensor head_out, void* stream);
-/* 1 when dbsr_conv2d_head accepts `d`: pipelined shape (bf16 3x3/s1/p1, width % 64 == 0, height % 8 == 0,
- * >= 256 tiles), cout == 32, residual, act none, post-act ReLU. */
+/* 1 when dbsr_conv2d_head accepts `d`: pipelined shape (16-bit 3x3/s1/p1, width % 64 == 0, height % 8 == 0,
+ * >= 256 tiles), cout == 32, residual, act none, post-act ReLU.  (The engine prefers dbsr_resblock_head, the whole
+ * last post-ResBlock + head in one launch, where dbsr_resblock_ok serves the shape.) */
 int dbsr_conv_head_ok(const dbsr_conv_desc* d);
 /* Scratch bytes dbsr_conv2d would use for split-K on `d` (0 = no split).  Convs whose grid cannot fill
  * the chip split K into slices that store fp32 partials to `workspace`; a second launch sums them in
@@ -205,7 +207,7 @@ int dbsr_fuse_softmax(int B, int N, int hw, int c, dbsr_tensor logits, dbsr_tens
  * 128 channels) super-tile keeps all N frames' fp32 logits in its waves' accumulators; weights = softmax over
  * the N frames (fp32, stored in the conv dtype), fused = sum_n weights * features (fp32, stored in the dtype).
  * ref / oth / fused / weights address as in dbsr_fuse_softmax (c = d->cout; weights.ptr NULL: no aux output);
- * d->y, d->res are unused; d->max_blocks caps the persistent grid.  Requires dbsr_conv_fuse_ok(d, B, N):
+ * d->y, d->res are unused; d->max_blocks caps the persistent grid (rounded down to a multiple of 8, at least 8).  Requires dbsr_conv_fuse_ok(d, B, N):
  * 16-bit 3x3/s1/p1/d1, cin > 16, cout % 128 == 0 (<= 512), d->n_frames == B*N, N == 14, width % 16 == 0,
  * height % 2 == 0, and frame maps affine in (burst, frame); the feature / output tensors need ld and c0
  * multiples of 8 with c0 + cout <= ld (DBSR_E_ARG otherwise). */

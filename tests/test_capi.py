@@ -174,9 +174,35 @@ def test_lds_dma_kernels_own_their_simds():
     spec = importlib.util.spec_from_file_location('isa_audit', os.path.join(repo, 'tools', 'isa_audit.py'))
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
-    rows, bad = mod.audit(os.path.join(repo, 'deep-rawburst-sr_amd', 'libdbsr_hip.so'))
+    hazards = []
+    rows, bad = mod.audit(os.path.join(repo, 'deep-rawburst-sr_amd', 'libdbsr_hip.so'), hazards)
     assert len(rows) >= 40, 'expected the pipelined / weight-stationary / tiled LDS-DMA kernels'
+    assert not hazards, hazards[:5]
     assert not bad, bad
+
+
+def _isa_audit():
+    import importlib.util
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location('isa_audit', os.path.join(repo, 'tools', 'isa_audit.py'))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_isa_audit_store_data_hazard_rule():
+    """The store-data hazard rule (the ROCm 7.2 finding of DESIGN.md f2) on hand-written sequences:
+    a VALU write to a store's data VGPRs right after it is flagged, for buffer and global stores; wait states
+    (s_nop, other instructions) or disjoint registers clear it."""
+    hz = _isa_audit().store_data_hazards
+    assert hz(['buffer_store_dwordx4 v[4:7], v1, s[0:3], 0 offen', 'v_pk_mul_f32 v[4:5], v[8:9], v[10:11]'])
+    assert hz(['global_store_dwordx4 v2, v[4:7], s[0:1]', 'v_mov_b32_e32 v6, 0'])
+    assert hz(['global_store_dwordx4 v[2:3], v[4:7], off', 's_nop 0', 'v_add_f32_e32 v7, v1, v2'])
+    assert not hz(['buffer_store_dwordx4 v[4:7], v1, s[0:3], 0 offen', 's_nop 1', 'v_pk_mul_f32 v[4:5], v[8:9], v[10:11]'])
+    assert not hz(['global_store_dwordx4 v2, v[4:7], s[0:1]', 'v_mov_b32_e32 v8, 0', 'v_mov_b32_e32 v9, 0',
+                   'v_mov_b32_e32 v5, 0'])
+    assert not hz(['global_store_dwordx4 v2, v[4:7], s[0:1]', 'v_mov_b32_e32 v2, 0'])     # the address, not data
+    assert not hz(['buffer_store_dwordx4 v[4:7], v1, s[0:3], 0 offen', 'v_cmp_gt_f32_e32 vcc, v4, v5'])
 
 
 def _cfg4_decoder_descs(L, rows, full=96, W=96, s=16):
@@ -343,3 +369,43 @@ def test_shuffle_blur_ok_accepts_and_rejects(L):
     assert ok(_shuffle_conv(L, 8, 48, 48, 64, dtype=L.DBSR_F32)) == 0
     assert ok(_shuffle_conv(L, 8, 48, 48, 64, y_ld=40, y_c0=12)) == 0   # unaligned slice
     assert ok(_shuffle_conv(L, 8, 48, 48, 64, y_ld=48, y_c0=24)) == 0   # slice past ld
+
+
+def _rb_pair(L, x_ptr, y_ptr, n=2, h=32, w=64, ld=32):
+    """conv1 / conv2 descs of a 32-channel ResBlock x -> y (host-only: fake device addresses)."""
+    ident = L.FrameMap(1, 1, 0, 1)
+
+    def conv(xp, yp, act, res=None, post=L.ACT_NONE):
+        d = L.ConvDesc()
+        d.n_frames = n
+        d.x = L.Tensor(xp, L.DBSR_F16, h * w * ld, ld, 0, ident)
+        d.in_h, d.in_w, d.out_h, d.out_w = h, w, h, w
+        d.cin, d.cout, d.kh, d.kw, d.stride, d.pad, d.dil = 32, 32, 3, 3, 1, 1, 1
+        d.w = 1 << 20
+        d.y = L.Tensor(yp, L.DBSR_F16, h * w * ld, ld, 0, ident)
+        d.act, d.post_act = act, post
+        d.res = res if res is not None else L.NULL_TENSOR
+        d.gate = L.NULL_TENSOR
+        d.out_mode = L.OUT_NHWC
+        return d
+    mid = 1 << 40
+    c1 = conv(x_ptr, mid, L.ACT_RELU)
+    c2 = conv(mid, y_ptr, L.ACT_NONE, res=L.Tensor(x_ptr, L.DBSR_F16, h * w * ld, ld, 0, ident), post=L.ACT_RELU)
+    return c1, c2
+
+
+def test_resblock_rejects_output_aliasing_input(L):
+    """the persistent ResBlock kernel reads neighbouring tiles' halos of x while other blocks
+    store y, so an output overlapping x is refused by dbsr_resblock_ok and by dbsr_resblock (DBSR_E_ARG, before
+    any launch); disjoint buffers are accepted."""
+    lib = L.lib()
+    nbytes = 2 * 32 * 64 * 32 * 2                         # 2 frames of 32x64 pixels x 32 ch x 2 B
+    x = 1 << 32
+    ok = lambda c1, c2: lib.dbsr_resblock_ok(ctypes.byref(c1), ctypes.byref(c2))   # noqa: E731
+    assert ok(*_rb_pair(L, x, x + nbytes)) == 1                               # adjacent, disjoint
+    assert ok(*_rb_pair(L, x, x)) == 0                                        # in place
+    assert ok(*_rb_pair(L, x, x + nbytes - 64)) == 0                          # last pixel overlaps
+    assert ok(*_rb_pair(L, x + nbytes - 64, x)) == 0                          # y's tail under x's head
+    c1, c2 = _rb_pair(L, x, x)
+    assert lib.dbsr_resblock(ctypes.byref(c1), ctypes.byref(c2), None) == -1                 # DBSR_E_ARG
+    assert b'overlap' in lib.dbsr_last_error()

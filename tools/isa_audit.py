@@ -11,6 +11,12 @@ race'): every kernel that issues LDS-DMA (buffer_load_* ... lds / glo
     workgroup that ends with pieces outstanding frees its LDS to the next workgroup while they land (VERDICT r4
     #6, e.g. a persistent block's prefetch past its last tile).
 
+Over EVERY kernel (LDS-DMA or not): no VALU instruction may overwrite the data VGPRs of a vector-memory store
+(buffer_/global_/flat_store_*) within STORE_HAZARD_WAIT wait states of it -- the store may not have read its data
+yet.  ROCm 7.2 emitted a v_pk_mul_f32 straight after a buffer_store over its data registers with no s_nop between
+(the fused predictor's fusion weights came out corrupted at fixed lanes); the product avoids
+buffer_store and builds that file with -fno-slp-vectorize, and this rule guards the class.
+
 Usage: python tools/isa_audit.py [libdbsr_hip.so]   (prints one line per LDS-DMA kernel; exit 1 on a violation)
 Also imported by tests/test_capi.py."""
 import os
@@ -29,6 +35,54 @@ DMA_RE = re.compile(r'\b(buffer_load_\w+\b.*\blds\b|global_load_lds_\w+)')
 # wave's last DMA and every barrier.  Its 9-wave blocks cannot own their SIMDs (3 waves on one SIMD); it is a
 # training-step kernel, issued on the trainer's one stream (no second lane runs beside the backward).
 RING_KERNELS = ('conv_wgrad_dma_kernel', 'conv_fuse_kernel')
+# wait states a store's data VGPRs must stay untouched by VALU writes after the store issues (the CDNA3/4 ISA's
+# "VMEM store data hazard", stores of more than 64 bits of data: 1 wait state; 2 here, a margin for gfx950's
+# packed-fp32 VALU, whose write was the one observed racing)
+STORE_HAZARD_WAIT = 2
+STORE_RE = re.compile(r'^(buffer|global|flat|scratch)_store_\w+\s+(?:off,\s*)?')
+VREG_RE = re.compile(r'\bv(?:\[(\d+):(\d+)\]|(\d+)\b)')
+
+
+def _vregs(op):
+    """The VGPR indices an operand names (vN or v[a:b]), else an empty set."""
+    m = VREG_RE.match(op.strip())
+    if not m:
+        return set()
+    if m.group(3) is not None:
+        return {int(m.group(3))}
+    return set(range(int(m.group(1)), int(m.group(2)) + 1))
+
+
+def store_data_hazards(ins):
+    """[(store, valu)] pairs: a VALU write to a store's data VGPRs within STORE_HAZARD_WAIT wait states of it.
+    Store operands: global/flat/scratch_store vaddr, vdata, ...; buffer_store vdata, vaddr, ..."""
+    out = []
+    for j, t in enumerate(ins):
+        m = re.match(r'^(buffer|global|flat|scratch)_store_(\w+)\s+(.*)$', t)
+        # the hazard exists for stores of more than 64 bits of data (dwordx3 / dwordx4, b96 / b128)
+        if not m or not re.match(r'(dwordx[34]|b96|b128)', m.group(2)):
+            continue
+        ops = [o.strip() for o in m.group(3).split(',')]
+        data = _vregs(ops[0] if m.group(1) == 'buffer' else (ops[1] if len(ops) > 1 else ''))
+        if not data:
+            continue
+        waited, q = 0, j + 1
+        while q < len(ins) and waited < STORE_HAZARD_WAIT:
+            u = ins[q]
+            if re.match(r'^(s_endpgm|s_branch|s_setpc)', u):
+                break                   # no fall-through: the next instruction in code order does not follow it
+            n = re.match(r'^s_nop\s+(\w+)', u)
+            if n:
+                waited += int(n.group(1), 0) + 1
+            else:
+                if u.startswith('v_') and not re.match(r'^v_(readlane|readfirstlane|cmp|cmpx)', u):
+                    dst = u.split(None, 1)[1].split(',')[0] if ' ' in u else ''
+                    if _vregs(dst) & data:
+                        out.append((t, u))
+                        break
+                waited += 1
+            q += 1
+    return out
 
 
 def code_objects(so_path):
@@ -77,7 +131,9 @@ def kernel_meta(co_file):
     return meta
 
 
-def audit(so_path):
+def audit(so_path, hazards=None):
+    """rows / bad kernels of the LDS-DMA rules; `hazards` (a list, optional) collects (kernel, store, valu) store-data
+    hazards over every kernel -- their kernels are added to `bad` too."""
     rows, bad = [], []
     with tempfile.TemporaryDirectory() as td:
         for i, co in enumerate(code_objects(so_path)):
@@ -99,6 +155,14 @@ def audit(so_path):
                 if k not in meta:
                     continue
                 ins = [ln.split(';')[0].strip() for ln in lines if ln.strip()]
+                # objdump lines: '<tab>mnemonic operands  // address: encoding' -- keep the instruction text only
+                ins = [t.split('//')[0].strip() for t in ins]
+                ins = [t for t in ins if t]
+                hz = store_data_hazards(ins)
+                if hz:
+                    bad.append(k)
+                    if hazards is not None:
+                        hazards.extend((k, st, va) for st, va in hz)
                 dma = [j for j, t in enumerate(ins) if DMA_RE.search(t)]
                 if not dma:
                     continue
@@ -155,11 +219,14 @@ def audit(so_path):
 def main():
     so = sys.argv[1] if len(sys.argv) > 1 else os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                              'deep-rawburst-sr_amd', 'libdbsr_hip.so')
-    rows, bad = audit(so)
+    hazards = []
+    rows, bad = audit(so, hazards)
+    for k, st, va in hazards:
+        print('STORE-DATA HAZARD %s: %s  <-  %s' % (k[:90], st, va))
     for k, n, regs, hv, ha, lds, wg, owns, m0, dec, fits, drain, end in rows:
         print('%-90s dma %3d regs %3d (max v%d a%d) lds %6d wg %3d owns %d m0 %d declared %d lds-ok %d drain %d '
               'end %d' % (k[:90], n, regs, hv, ha, lds, wg, owns, m0, dec, fits, drain, end))
-    print('%d LDS-DMA kernels, %d violations' % (len(rows), len(bad)))
+    print('%d LDS-DMA kernels, %d store-data hazards, %d violations' % (len(rows), len(hazards), len(set(bad))))
     sys.exit(1 if bad else 0)
 
 

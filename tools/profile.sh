@@ -11,10 +11,10 @@ mkdir -p $out
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace -o run --output-format csv -- \
     python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-op-timing > $out/bench_trace.log 2>&1 || exit $?
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "warp512|warp_kernel|fuse_softmax|fuse512|conv3x3|conv1x1|upsample_shuffle|pwc_dense|pwc_extract" \
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "warp512|warp_kernel|fuse_softmax|fuse512|conv3x3|conv1x1|upsample_shuffle|upsample_blur|resblock32|conv_fuse|conv2d_kernel|pwc_dense|pwc_extract" \
     -d $out/pmc_fetch -o run --output-format csv -- \
     python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-op-timing > $out/bench_fetch.log 2>&1 || exit $?
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "warp512|warp_kernel|fuse_softmax|fuse512|conv3x3|conv1x1|upsample_shuffle|pwc_dense|pwc_extract" \
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "warp512|warp_kernel|fuse_softmax|fuse512|conv3x3|conv1x1|upsample_shuffle|upsample_blur|resblock32|conv_fuse|conv2d_kernel|pwc_dense|pwc_extract" \
     -d $out/pmc_write -o run --output-format csv -- \
     python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-op-timing > $out/bench_write.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/train -o run --output-format csv -- \

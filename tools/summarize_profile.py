@@ -17,8 +17,10 @@ import sys
 KERNELS = {   # label -> (name predicate, algorithmic bytes per launch at the default bench workload)
     'warp kernel (DBSR warp, encoders.py:80)':
         (lambda n: ('warp_kernel' in n and 'backwarp' not in n and '_bwd' not in n) or 'warp512_bf16_kernel' in n, None),
-    'fusion kernel (merging.py:116-126)': (lambda n: 'fuse_softmax_kernel' in n or 'fuse512_bf16_kernel' in n, None),
-    'conv3x3_pipe_kernel, largest grid (wp.out 128->512)': (lambda n: 'conv3x3_pipe_kernel<' in n and '64, 48, 8, 3>' in n, None),
+    'fused wp.out conv + softmax + fusion (merging.py:55-57,116-126)': (lambda n: 'conv_fuse_kernel' in n, None),
+    'fused 32-ch ResBlock (decoders.py:46-49)': (lambda n: 'resblock32_kernel' in n and ('Lb0E' in n or 'false>' in n), None),
+    'fused 32-ch ResBlock + RGB predictor (decoders.py:59-61)': (lambda n: 'resblock32_kernel' in n and ('Lb1E' in n or 'true>' in n), None),
+    'upsampler conv + PixelShuffle + blur (upsampling.py:51-66)': (lambda n: 'upsample_blur_kernel' in n, None),
 }
 
 
@@ -26,7 +28,9 @@ KERNELS = {   # label -> (name predicate, algorithmic bytes per launch at the de
 FAMILY = [('conv3x3_ws_kernel', 'conv3x3_ws'), ('conv3x3_pipe_kernel', 'conv3x3_pipe'),
           ('conv3x3_tiled_kernel', 'conv3x3_tiled'), ('conv3x3_narrow_kernel', 'conv3x3_narrow'),
           ('conv1x1_kernel', 'conv1x1'),
-          ('upsample_shuffle_kernel', 'conv1x1_shuffle'), ('pwc_dense', 'pwc_dense'),
+          ('upsample_shuffle_kernel', 'conv1x1_shuffle'), ('upsample_blur_kernel', 'conv1x1_shuffle_blur'),
+          ('resblock32_kernel', 'resblock32'), ('conv_fuse_kernel', 'conv_fuse'), ('conv2d_kernel', 'conv2d_generic'),
+          ('pwc_dense', 'pwc_dense'),
           ('pwc_extract_kernel', 'pwc_extract'), ('warp512_bf16_kernel', 'warp'), ('fuse512_bf16_kernel', 'fuse')]
 
 
