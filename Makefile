@@ -19,7 +19,7 @@ TORCH_FLAGS := --offload-arch=$(ARCH) -O2 -std=c++17 -fPIC -D_GLIBCXX_USE_CXX11_
 
 all: $(LIB) $(TORCH_LIB)
 
-$(OBJDIR)/%.o: $(SRC)/%.hip $(SRC)/common.hpp include/dbsr_hip.h
+$(OBJDIR)/%.o: $(SRC)/%.hip $(SRC)/common.hpp $(SRC)/conv_core.hpp include/dbsr_hip.h
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(FLAGS) -c $< -o $@
 

@@ -36,7 +36,8 @@ PEAK_MFMA_TFLOPS = {'bf16': 2500.0, 'fp16': 2500.0, 'fp32': 157.3}   # dense pea
 DTYPES = {'bf16': 'bfloat16', 'fp16': 'float16', 'fp32': 'float32'}
 # conv-like kernel families (MFMA-bound; bench reports each against the dense peak)
 CONV_FAMILIES = ('conv3x3_ws', 'conv3x3_pipe', 'conv3x3_tiled', 'conv3x3_narrow', 'conv2d_generic', 'conv1x1',
-                 'conv1x1_shuffle', 'conv1x1_shuffle_blur', 'resblock32', 'conv_fuse', 'pwc_dense', 'pwc_extract')
+                 'conv1x1_shuffle', 'conv1x1_shuffle_blur', 'resblock32', 'resblock64', 'conv_fuse', 'pwc_dense',
+                 'pwc_extract')
 KERNEL_DESC = {'conv3x3_ws': 'conv3x3_ws_kernel (persistent weight-stationary implicit-GEMM 3x3, Cin <= 64',
                'conv3x3_pipe': 'conv3x3_pipe_kernel (persistent LDS-DMA-pipelined implicit-GEMM 3x3',
                'conv3x3_tiled': 'conv3x3_tiled_kernel (LDS-tiled implicit-GEMM 3x3',
@@ -46,6 +47,8 @@ KERNEL_DESC = {'conv3x3_ws': 'conv3x3_ws_kernel (persistent weight-stationary im
                'conv1x1_shuffle': 'upsample_shuffle_kernel (1x1 conv + PixelShuffle',
                'conv1x1_shuffle_blur': 'upsample_blur_kernel (1x1 conv + PixelShuffle + 3x3 Gaussian blur',
                'resblock32': 'resblock32_kernel (a whole 32-channel ResBlock, intermediate in the LDS',
+               'resblock64': 'resblock64_kernel (a whole 64-channel ResBlock: conv1 / conv2 wave roles pipelined over '
+                             'tiles, intermediate in the LDS',
                'conv_fuse': 'conv_fuse_kernel (weight-predictor output conv + softmax + fusion',
                'pwc_dense': 'pwc_dense_kernel (PWC-Net DenseNet decoder level in one launch',
                'pwc_extract': 'pwc_extract_kernel (PWC-Net feature pyramid in one launch'}
@@ -394,6 +397,7 @@ def main():
                       'note': 'algorithmic bytes per launch = ' + {
                           'conv_fuse': 'hidden input + the N frames\' features + fusion weights + fused output',
                           'resblock32': 'x in + y (or the fused head\'s fp32 RGB) out',
+                          'resblock64': 'x in + y out',
                           'conv1x1_shuffle_blur': 'low-res input + blurred high-res output'}.get(k, '')}
         for k in ('warp', 'fuse'):
             if k in fam_chip:

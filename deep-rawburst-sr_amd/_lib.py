@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get('DBSR_HIP_LIB', os.path.join(_HERE, 'libdbsr_hip.so'))
 DBSR_F32, DBSR_BF16, DBSR_F16 = 0, 1, 2
 ACT_NONE, ACT_RELU, ACT_LRELU = 0, 1, 2
 OUT_NHWC, OUT_SHUFFLE, OUT_NCHW_F32 = 0, 1, 2
-ABI_VERSION = 18
+ABI_VERSION = 19
 
 
 class FrameMap(ctypes.Structure):
@@ -76,6 +76,7 @@ def lib():
             'dbsr_abi_version': ([], c_int),
             'dbsr_last_error': ([], ctypes.c_char_p),
             'dbsr_conv_packed_elems': ([c_int, c_int, c_int, c_int], c_size_t),
+            'dbsr_weights_round_diffuse': ([c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p], c_int),
             'dbsr_conv_pack_weights': ([c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
                                         c_void_p, c_void_p], c_int),
             'dbsr_conv2d': ([ctypes.POINTER(ConvDesc), c_void_p], c_int),
@@ -167,7 +168,8 @@ def lib():
     return _lib
 
 
-EXPORTED = ['dbsr_abi_version', 'dbsr_last_error', 'dbsr_conv_packed_elems', 'dbsr_conv_pack_weights', 'dbsr_conv2d',
+EXPORTED = ['dbsr_abi_version', 'dbsr_last_error', 'dbsr_conv_packed_elems', 'dbsr_conv_pack_weights',
+            'dbsr_weights_round_diffuse', 'dbsr_conv2d',
             'dbsr_set_conv_algo', 'dbsr_conv_kernel_for', 'dbsr_conv_dispatch_variant', 'dbsr_conv_lane_reach', 'dbsr_conv_workspace_bytes', 'dbsr_conv2d_head',
             'dbsr_conv_head_ok', 'dbsr_conv_shuffle_blur', 'dbsr_conv_shuffle_blur_ok', 'dbsr_resblock', 'dbsr_resblock_ok', 'dbsr_resblock_head',
             'dbsr_correlation', 'dbsr_correlation_backward', 'dbsr_backwarp', 'dbsr_warp_bilinear', 'dbsr_fuse_softmax',

@@ -16,7 +16,7 @@
 // kernel serves every conv of the path: ResNet 3x3, 1x1 projections, strided PWC extractor,
 // dilated refiner, the DenseNet decoder (channel-slice reads/writes into one buffer: no cat), the
 // ResBlock residual (+ReLU) and the PixelShuffle epilogue of the decoder upsampler.
-#include "common.hpp"
+#include "conv_core.hpp"
 
 #include <algorithm>
 #include <type_traits>
@@ -28,35 +28,7 @@ using namespace dbsr;
 
 namespace {
 
-inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
-// channel padding of the packed K dimension (dbsr_hip.h): 8 for cin <= 16, else 32, so every
-// conv with cin > 16 is a whole number of 32-channel MFMA chunks per tap
-inline int cin_pad(int cin) { return cin <= 16 ? round_up(cin, 8) : round_up(cin, 32); }
-
 int g_tiled_enabled = 1;
-inline bool is16(int dtype) { return dtype == DBSR_BF16 || dtype == DBSR_F16; }   // 16-bit activations
-inline int esize(int dtype) { return is16(dtype) ? 2 : 4; }   // dbsr_set_conv_algo: 0 generic only, 1 LDS-tiled where applicable, 2 + pipelined
-
-struct ConvK {
-    const void* x; long long x_is; int x_ld; dbsr_frame_map xm; int in_h, in_w;
-    const void* w; const float* bias; int Kp, KG, KGp, CG, kw, stride, pad, dil, cout;
-    void* y; int y_f32; long long y_is; int y_ld, y_c0; dbsr_frame_map ym; int out_h, out_w;
-    int act;
-    const void* r; long long r_is; int r_ld, r_c0; dbsr_frame_map rm; int post_act;
-    const void* gt; long long g_is; int g_ld, g_c0; dbsr_frame_map gm;   // gate (ReLU backward): out *= (gate > 0)
-    int out_mode, shuffle, cps;
-    int npix;
-    int vec_store;
-    int ksplit;        // K slices (generic kernel); > 1: fp32 partials to ws, summed by conv_splitk_finalize
-    float* ws;         // [ksplit][npix][cw] fp32
-    int cw;            // round_up(cout, 4)
-    const void* w_pipe;  // chunk-major weight copy (3x3, cin > 16): [cout/16][chunk][tap][4 k-groups][16 co][8]
-    int max_blocks;      // persistent kernel: workgroup cap (0 = one per CU)
-    const float* head_w; // fused 1x1 head (pipelined kernel, EPI 4): fp32 [head_cout][cout], bias [head_cout]
-    const float* head_b;
-    int head_cout;       // y is then the head's fp32 NCHW output (y_is = image stride)
-    int stage_epi;       // generic kernel, MT == 4: LDS-staged 16-B-row epilogue (set by launch_conv)
-};
 
 // The geometry every dispatch decision is taken on: `d` itself, or (d->plan_h > 0) `d` as if its image were
 // plan_h output rows tall -- a frame-sharded rank's decoder slab then takes the whole image's kernels, tiles
@@ -82,56 +54,6 @@ __host__ __device__ __forceinline__ int pipe_lane_ch(int cb, int h, int g, int c
 __host__ __device__ __forceinline__ int ws_lane_ch(int ctb, int wc, int g, int cout) {
     const int c = ctb + 32 * wc + 8 * g;
     return c < cout ? c : ctb;
-}
-
-template <typename T> struct Frag;
-template <> struct Frag<bf16_t> {
-    bf16x8_t v;
-    __device__ __forceinline__ void load(const bf16_t* p) { v = *(const bf16x8_t*)p; }
-    __device__ __forceinline__ void zero() { v = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0}; }
-};
-template <> struct Frag<f16_t> {
-    bf16x8_t v;                                                 // raw fp16 bits
-    __device__ __forceinline__ void load(const f16_t* p) { v = *(const bf16x8_t*)p; }
-    __device__ __forceinline__ void zero() { v = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0}; }
-};
-template <> struct Frag<float> {
-    float4 a, b;
-    __device__ __forceinline__ void load(const float* p) { a = *(const float4*)p; b = *(const float4*)(p + 4); }
-    __device__ __forceinline__ void load(const bf16_t* p) {      // bf16 activations, fp32 ("precise") math
-        const u32x4_t q = *(const u32x4_t*)p;
-        a = make_float4(__uint_as_float(q[0] << 16), __uint_as_float(q[0] & 0xffff0000u),
-                        __uint_as_float(q[1] << 16), __uint_as_float(q[1] & 0xffff0000u));
-        b = make_float4(__uint_as_float(q[2] << 16), __uint_as_float(q[2] & 0xffff0000u),
-                        __uint_as_float(q[3] << 16), __uint_as_float(q[3] & 0xffff0000u));
-    }
-    __device__ __forceinline__ void load(const f16_t* p) {       // fp16 activations, fp32 ("precise") math
-        const u32x4_t q = *(const u32x4_t*)p;
-        a = make_float4(H16<f16_t>::lo(q[0]), H16<f16_t>::hi(q[0]), H16<f16_t>::lo(q[1]), H16<f16_t>::hi(q[1]));
-        b = make_float4(H16<f16_t>::lo(q[2]), H16<f16_t>::hi(q[2]), H16<f16_t>::lo(q[3]), H16<f16_t>::hi(q[3]));
-    }
-    __device__ __forceinline__ void zero() { a = make_float4(0, 0, 0, 0); b = a; }
-};
-
-__device__ __forceinline__ f32x4_t mma(const Frag<bf16_t>& A, const Frag<bf16_t>& B, f32x4_t c) {
-    typedef __attribute__((ext_vector_type(8))) __bf16 bfv;
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bfv, A.v), __builtin_bit_cast(bfv, B.v), c,
-                                                   0, 0, 0);
-}
-__device__ __forceinline__ f32x4_t mma(const Frag<f16_t>& A, const Frag<f16_t>& B, f32x4_t c) {
-    typedef __attribute__((ext_vector_type(8))) _Float16 hv;
-    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(hv, A.v), __builtin_bit_cast(hv, B.v), c, 0, 0, 0);
-}
-__device__ __forceinline__ f32x4_t mma(const Frag<float>& A, const Frag<float>& B, f32x4_t c) {
-    c = __builtin_amdgcn_mfma_f32_16x16x4f32(A.a.x, B.a.x, c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_16x16x4f32(A.a.y, B.a.y, c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_16x16x4f32(A.a.z, B.a.z, c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_16x16x4f32(A.a.w, B.a.w, c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_16x16x4f32(A.b.x, B.b.x, c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_16x16x4f32(A.b.y, B.b.y, c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_16x16x4f32(A.b.z, B.b.z, c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_16x16x4f32(A.b.w, B.b.w, c, 0, 0, 0);
-    return c;
 }
 
 // bias of output channels co..co+3, loaded unconditionally from clamped indices (a per-element
@@ -883,14 +805,6 @@ struct PipeCfg {
 // pixels x 64 B, i.e. 16 cache lines per wave-instruction instead of the 64 of a planar [k-group][pixel]
 // piece, and the swizzle keeps every B-fragment ds_read_b128 conflict-free for any tap shift: within
 // each of its four 16-lane groups, the 4 lanes with equal p mod 4 read 4 distinct phys values.
-// ReLU of two packed 16-bit floats (bf16 or fp16) on their bit patterns: a signed 16-bit max with 0 zeroes every
-// negative value and -0, so relu16x2(pack(x)) == pack(max(x, 0)) bitwise
-__device__ __forceinline__ unsigned relu16x2(unsigned v) {
-    typedef short s16x2 __attribute__((ext_vector_type(2)));
-    return __builtin_bit_cast(unsigned, __builtin_elementwise_max(__builtin_bit_cast(s16x2, v), s16x2{0, 0}));
-}
-__device__ __forceinline__ int halo_phys(int p, int g) { return 2 * (g & 1) + ((g >> 1) ^ ((p >> 2) & 1)); }
-
 // Diagnostic build only (make exp EXP_FLAGS=-DDBSR_PIPE_STAMPS): per-wave s_memtime stamps around each
 // stage's barrier and tap loop, read back by dbsr_diag_pipe_stamps (tools/pipe_stamps.py).  The product
 // build compiles none of this.
@@ -1712,14 +1626,6 @@ constexpr int LDS_BYTES = (2 * IN_U4 + MID_U4) * 16 + 64 * 4;
 static_assert(LDS_BYTES <= 160 * 1024, "resblock LDS");
 }  // namespace rbk
 
-// tile of block b's round i (blocks b < ntiles % nb take one round more): a full round of 256 tiles goes to the
-// 256 blocks so that XCD b % 8 takes 32 consecutive tiles; a partial last round in block order (its tiles exist
-// only for b < ntiles % nb -- applied to it, the XCD order addressed tiles past the last frame)
-__host__ __device__ __forceinline__ int rb_tile(int i, int b, int nb, int ntiles) {
-    if (nb == 256 && (i + 1) * 256 <= ntiles) return i * 256 + (b & 7) * 32 + (b >> 3);
-    return i * nb + b;
-}
-
 // HEAD: the decoder's RGB predictor (decoders.py:61, 1x1 32 -> head_cout + ReLU) on the block's fp32 output, as
 // the pipelined kernel's epilogue 4 computes it (same products, order and lane reduction); k2.y is then the
 // head's fp32 NCHW output and the block's own output is not stored
@@ -1965,20 +1871,6 @@ __global__ __launch_bounds__(512, 1) void resblock32_kernel(ConvK k1, ConvK k2, 
     vm_drain();                         // (no LDS-DMA outstanding at s_endpgm: tools/isa_audit.py)
 }
 
-// every (block, round) of a launch maps to a distinct tile below ntiles (checked on the host before each launch)
-bool rb_mapping_ok(int nb, int ntiles) {
-    std::vector<unsigned char> seen(ntiles, 0);
-    for (int b = 0; b < nb; ++b) {
-        const int my = ntiles / nb + (b < ntiles % nb ? 1 : 0);
-        for (int i = 0; i < my; ++i) {
-            const int t = rb_tile(i, b, nb, ntiles);
-            if (t < 0 || t >= ntiles || seen[t]) return false;
-            seen[t] = 1;
-        }
-    }
-    return true;
-}
-
 // byte range [lo, hi) that `n` frames of t cover: each stored image from its first used element (c0) to the last
 // pixel's last element (per_img elements past the image base: NHWC (hw - 1) * ld + c0 + ch, NCHW its plane count)
 void tensor_span(const dbsr_tensor& t, int n, long long per_img, int es, unsigned long long& lo,
@@ -2000,35 +1892,48 @@ void tensor_span(const dbsr_tensor& t, int n, long long per_img, int es, unsigne
 bool resblock_out_disjoint(const dbsr_conv_desc* c1, const dbsr_conv_desc* c2, const dbsr_tensor* head_out,
                            int head_cout) {
     const long long hw = (long long)c1->in_h * c1->in_w;
+    const int C = c1->cin;
     unsigned long long xl, xh, yl, yh;
-    tensor_span(c1->x, c1->n_frames, (hw - 1) * c1->x.ld + c1->x.c0 + 32, 2, xl, xh);
+    tensor_span(c1->x, c1->n_frames, (hw - 1) * c1->x.ld + c1->x.c0 + C, 2, xl, xh);
     if (head_out) tensor_span(*head_out, c1->n_frames, (long long)head_cout * hw, 4, yl, yh);
-    else tensor_span(c2->y, c1->n_frames, (hw - 1) * c2->y.ld + c2->y.c0 + 32, 2, yl, yh);
+    else tensor_span(c2->y, c1->n_frames, (hw - 1) * c2->y.ld + c2->y.c0 + C, 2, yl, yh);
     return yh <= xl || xh <= yl;
 }
 
 // the fused ResBlock applies: c1 = conv1 (x -> any, ReLU), c2 = conv2 (-> y, residual x, post-ReLU), both
-// 16-bit 3x3/s1/p1/d1 32 -> 32 with chunk-major weight copies, frames a multiple of 32 x 16, NHWC slices aligned
-bool use_resblock32(const dbsr_conv_desc* c1, const dbsr_conv_desc* c2) {
-    auto conv_ok = [](const dbsr_conv_desc* d) {
+// 16-bit 3x3/s1/p1/d1 C -> C with chunk-major weight copies, NHWC slices aligned; returns C (32: resblock32_kernel,
+// frames a multiple of 32 x 16; 64: resblock64_kernel, frames a multiple of 16 x 16) or 0
+int resblock_channels(const dbsr_conv_desc* c1, const dbsr_conv_desc* c2) {
+    if (!c1 || !c2) return 0;
+    const int C = c1->cin;
+    if (C != 32 && C != 64) return 0;
+    auto conv_ok = [C](const dbsr_conv_desc* d) {
         return is16(d->x.dtype) && d->y.dtype == d->x.dtype && !d->precise && d->kh == 3 && d->kw == 3 &&
-               d->stride == 1 && d->pad == 1 && d->dil == 1 && d->cin == 32 && d->cout == 32 &&
+               d->stride == 1 && d->pad == 1 && d->dil == 1 && d->cin == C && d->cout == C &&
                d->out_mode == DBSR_OUT_NHWC && !d->gate.ptr && d->in_h == d->out_h && d->in_w == d->out_w;
     };
-    if (!c1 || !c2 || !conv_ok(c1) || !conv_ok(c2)) return false;
+    if (!conv_ok(c1) || !conv_ok(c2)) return 0;
     if (c1->act != DBSR_ACT_RELU || c1->res.ptr || c2->act != DBSR_ACT_NONE || c2->post_act != DBSR_ACT_RELU)
-        return false;
+        return 0;
     // the residual is conv1's input (same tensor, slice and frames)
     if (c2->res.ptr != c1->x.ptr || c2->res.c0 != c1->x.c0 || c2->res.ld != c1->x.ld ||
         c2->res.img_stride != c1->x.img_stride || c2->res.dtype != c1->x.dtype ||
         std::memcmp(&c2->res.map, &c1->x.map, sizeof(dbsr_frame_map)) != 0)
-        return false;
+        return 0;
     if (c1->n_frames != c2->n_frames || c1->in_h != c2->in_h || c1->in_w != c2->in_w || c1->x.dtype != c2->y.dtype)
-        return false;
-    if (c1->in_w % rbk::TW || c1->in_h % rbk::TH) return false;
-    if (c1->x.ld % 8 || c1->x.c0 % 8 || c1->x.c0 + 32 > c1->x.ld) return false;
-    if (c2->y.ld % 8 || c2->y.c0 % 8 || c2->y.c0 + 32 > c2->y.ld) return false;
-    return (long long)c1->in_h * c1->in_w * c1->x.ld * 2 < (1LL << 31);
+        return 0;
+    if (C == 32 ? (c1->in_w % rbk::TW || c1->in_h % rbk::TH) : (c1->in_w % rb64::TW || c1->in_h % rb64::TH)) return 0;
+    if (C == 64) {
+        // the 64-channel kernel only where it beats the two weight-stationary launches: small grids (the decoder's
+        // pre-ResBlocks, 144 tiles: 10.7 vs 12.1 us); at the encoder's 2016 tiles it measured 51 vs 49 us (uncapped)
+        // and 80 vs 69 us (under the 128-CU cap) -- DESIGN.md, round 6
+        const long long tiles = (long long)c1->n_frames * (c1->in_w / rb64::TW) * (c1->in_h / rb64::TH);
+        const int cus = c1->max_blocks > 0 ? std::min(c1->max_blocks, num_cus()) : num_cus();
+        if (tiles > 2LL * cus) return 0;
+    }
+    if (c1->x.ld % 8 || c1->x.c0 % 8 || c1->x.c0 + C > c1->x.ld) return 0;
+    if (c2->y.ld % 8 || c2->y.c0 % 8 || c2->y.c0 + C > c2->y.ld) return 0;
+    return (long long)c1->in_h * c1->in_w * c1->x.ld * 2 < (1LL << 31) ? C : 0;
 }
 
 template <typename T>
@@ -2960,7 +2865,7 @@ extern "C" int dbsr_conv2d(const dbsr_conv_desc* d, void* stream) {
 }
 
 extern "C" int dbsr_resblock_ok(const dbsr_conv_desc* c1, const dbsr_conv_desc* c2) {
-    return use_resblock32(c1, c2) && c2->y.ptr && resblock_out_disjoint(c1, c2, nullptr, 0) ? 1 : 0;
+    return resblock_channels(c1, c2) && c2->y.ptr && resblock_out_disjoint(c1, c2, nullptr, 0) ? 1 : 0;
 }
 
 int resblock_launch(const dbsr_conv_desc* c1, const dbsr_conv_desc* c2, const float* head_w, const float* head_b,
@@ -2968,10 +2873,19 @@ int resblock_launch(const dbsr_conv_desc* c1, const dbsr_conv_desc* c2, const fl
     DBSR_CHECK_ARG(c1 && c2 && c1->x.ptr && c1->w && c2->w, "resblock: null pointer");
     DBSR_CHECK_ARG(head_out || c2->y.ptr, "resblock: null output");
     DBSR_CHECK_ARG(c1->x.map.fpg > 0 && c2->y.map.fpg > 0 && c1->n_frames > 0, "resblock: bad frame map / sizes");
-    DBSR_CHECK_ARG(use_resblock32(c1, c2), "resblock: needs two 16-bit 3x3/s1/p1 32 -> 32 convs (conv1 ReLU; conv2 "
-                   "residual = conv1's input, post-ReLU), frames a multiple of 32 x 16, NHWC slices aligned to 8");
+    const int C = resblock_channels(c1, c2);
+    DBSR_CHECK_ARG(C, "resblock: needs two 16-bit 3x3/s1/p1 C -> C convs, C = 32 or 64 (conv1 ReLU; conv2 residual = "
+                   "conv1's input, post-ReLU), frames a multiple of 32 x 16 (C 32) / 16 x 16 (C 64), NHWC slices "
+                   "aligned to 8");
+    DBSR_CHECK_ARG(!head_out || C == 32, "resblock_head: 32-channel ResBlocks only");
     const ConvK k1 = make_convk(c1);
     ConvK k2 = make_convk(c2);
+    if (C == 64) {
+        DBSR_CHECK_ARG(resblock_out_disjoint(c1, c2, nullptr, 0),
+                       "resblock: the output must not overlap the input x (other blocks still read x's halos)");
+        return resblock64_launch(k1, k2, c1->n_frames, c1->x.dtype == DBSR_F16, c1->max_blocks, num_cus(),
+                                 (hipStream_t)stream);
+    }
     if (head_out) {
         DBSR_CHECK_ARG(head_w && head_out->ptr, "resblock_head: null pointer");
         DBSR_CHECK_ARG(head_cout >= 1 && head_cout <= 4, "resblock_head: head_cout must be 1..4");

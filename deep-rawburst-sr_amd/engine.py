@@ -143,9 +143,13 @@ class PackedConv:
     """One nn.Conv2d packed for dbsr_conv2d.  recipe() -> (weight, bias | None) gives the source tensors
     (default: the module's own); repack() re-packs them into the same buffers, so plans and captured graphs
     that point at them stay valid."""
-    def __init__(self, conv, dtype, device, stream, shuffle=1, recipe=None):
+    def __init__(self, conv, dtype, device, stream, shuffle=1, recipe=None, rounding='nearest'):
+        """rounding (16-bit dtypes): 'nearest' rounds each weight to its nearest 16-bit value; 'diffuse' rounds each
+        output channel's weights in K order with the running error carried (dbsr_weights_round_diffuse: the error
+        sum per channel stays within half an ulp, which the fp16 forward's error is most sensitive to)."""
         self.recipe = recipe or (lambda: (conv.weight, conv.bias))
         self.dtype, self.device, self.shuffle = dtype, device, shuffle
+        self.rounding = rounding if dtype in (torch.float16, torch.bfloat16) else 'nearest'
         w, b = self.recipe()
         self.cout, self.cin, self.kh, self.kw = w.shape
         self.stride, self.pad, self.dil = conv.stride[0], conv.padding[0], conv.dilation[0]
@@ -158,6 +162,12 @@ class PackedConv:
         w, b = self.recipe()
         w = w.detach().to(device=self.device, dtype=torch.float32).contiguous()
         b = b.detach().to(device=self.device, dtype=torch.float32).contiguous() if b is not None else None
+        if self.rounding == 'diffuse':
+            wr = torch.empty_like(w)
+            L.check(L.lib().dbsr_weights_round_diffuse(w.data_ptr(), self.cout, self.cin, self.kh, self.kw,
+                                                       L.dtype_code(self.dtype), wr.data_ptr(), stream),
+                    'dbsr_weights_round_diffuse')
+            w = wr                      # 16-bit-representable values: the pack's own rounding keeps them
         L.check(L.lib().dbsr_conv_pack_weights(w.data_ptr(), b.data_ptr() if b is not None else None, self.cout,
                                                self.cin, self.kh, self.kw, L.dtype_code(self.dtype), self.shuffle,
                                                self.w.data_ptr(),
@@ -287,16 +297,18 @@ class Plan:
         self.hbm[len(self.ops) - 1] = es * B * H * W * (N * d.cin + N * C + (N * C if weights.ptr else 0) + C)
         return len(self.ops) - 1
 
-    def resblock(self, name, c1, c2, n_frames, x, mid, y, hw, head=None):
-        """ResBlock (blocks.py:81-96) x -> y as one launch (dbsr_resblock: the intermediate stays in the LDS) when
-        the library serves it; returns False otherwise (the caller then emits conv1 into `mid` and conv2).
+    def resblock(self, name, c1, c2, n_frames, x, mid, y, hw, head=None, yc0=0):
+        """ResBlock (blocks.py:81-96) x -> y (channels from yc0) as one launch (dbsr_resblock: the intermediate stays
+        in the LDS; 32 channels: the decoder's post blocks, 64: the encoder / offset-feature / decoder pre blocks)
+        when the library serves it; returns False otherwise (the caller then emits conv1 into `mid` and conv2).
         head = (name, w [hc, 32] fp32, b | None, out_desc): the RGB predictor fused as well (dbsr_resblock_head;
         y is then not written)."""
         d1 = self._desc(name + '.conv1', c1, n_frames, x, 0, hw, mid, 0, L.ACT_RELU, IDENTITY, IDENTITY, None, 0,
                         IDENTITY, L.ACT_NONE, L.OUT_NHWC, 0, None, None, False, None, 0, IDENTITY)
-        d2 = self._desc(name + '.conv2', c2, n_frames, mid, 0, hw, y, 0, L.ACT_NONE, IDENTITY, IDENTITY, x, 0,
+        d2 = self._desc(name + '.conv2', c2, n_frames, mid, 0, hw, y, yc0, L.ACT_NONE, IDENTITY, IDENTITY, x, 0,
                         IDENTITY, L.ACT_RELU, L.OUT_NHWC, 0, None, None, False, None, 0, IDENTITY)
-        if not L.lib().dbsr_resblock_ok(ctypes.byref(d1), ctypes.byref(d2)):
+        if (c1.cout == 64 and not DBSREngine.FUSED_RESBLOCK64) or \
+                not L.lib().dbsr_resblock_ok(ctypes.byref(d1), ctypes.byref(d2)):
             return False
         self.convs.extend([(d1, self.lane), (d2, self.lane)])
         oh, ow = d1.out_h, d1.out_w
@@ -310,9 +322,10 @@ class Plan:
                      work=('flop', flop))
         else:
             self.add(name, L.lib().dbsr_resblock, ctypes.byref(d1), ctypes.byref(d2), work=('flop', flop))
-        self.kernel[len(self.ops) - 1] = 'resblock32'
-        # x in once; y out (16-bit, 32 ch) or the head's fp32 NCHW planes
-        self.hbm[len(self.ops) - 1] = n_frames * oh * ow * (2 * 32 + (4 * head[1].shape[0] if head is not None else 2 * 32))
+        self.kernel[len(self.ops) - 1] = 'resblock32' if c1.cout == 32 else 'resblock64'
+        # x in once; y out (16-bit) or the head's fp32 NCHW planes
+        self.hbm[len(self.ops) - 1] = n_frames * oh * ow * (2 * d1.cin + (4 * head[1].shape[0] if head is not None
+                                                                         else 2 * c2.cout))
         return True
 
     def conv_shuffle_blur(self, name, pc, n_frames, x, in_hw, y, act, k9):
@@ -475,11 +488,12 @@ class Plan:
 
 class _Weights:
     """All packed weights of a DBSRNet / PWCNet for one (dtype, device)."""
-    def __init__(self, dtype, device, stream):
-        self.dtype, self.device, self.stream = dtype, device, stream
+    def __init__(self, dtype, device, stream, rounding='nearest'):
+        self.dtype, self.device, self.stream, self.rounding = dtype, device, stream, rounding
 
     def conv(self, module, shuffle=1, recipe=None):
-        return PackedConv(module, self.dtype, self.device, self.stream, shuffle=shuffle, recipe=recipe)
+        return PackedConv(module, self.dtype, self.device, self.stream, shuffle=shuffle, recipe=recipe,
+                          rounding=self.rounding)
 
 
 def _param_signature(module):
@@ -666,14 +680,20 @@ class DBSREngine:
     FUSED_HEAD = True
     # PixelShuffle upsampler conv + shuffle + blur in one kernel (dbsr_conv_shuffle_blur)
     FUSED_UPSAMPLE_BLUR = True
-    # 32-channel ResBlocks (the decoder's post blocks) as one kernel each (dbsr_resblock)
+    # ResBlocks as one kernel each where the library serves them (dbsr_resblock: the decoder's 32-channel post blocks;
+    # the encoder's, the offset-feature extractor's and the decoder's 64-channel pre blocks)
     FUSED_RESBLOCK = True
+    FUSED_RESBLOCK64 = True   # (A/B switch for the 64-channel kernel alone)
     # weight-predictor input conv split into a per-frame [proj, offfeat] conv + a per-burst base conv
     LINEAR_SPLIT = True
     # weight-predictor output conv + softmax + fusion in one kernel (dbsr_conv_fuse_softmax: the fp32 logits never
     # reach memory) wherever the library serves the shape (16-bit, N = 14, cout % 128 == 0);
     # otherwise dbsr_conv2d into a logits buffer + dbsr_fuse_softmax
     FUSED_WP_OUT = True
+    # 16-bit weight rounding of the DBSR convs: 'diffuse' (dbsr_weights_round_diffuse: each output channel's rounding
+    # errors carried along its K, their sum within half an ulp) or 'nearest'.  At configs[1] the fp16 prediction's
+    # RMS error against the fp32 oracle: nearest 4.5e-4, diffuse 3.2e-4 (tools/precision_attrib.py)
+    WEIGHT_ROUNDING = 'diffuse'
 
     def __init__(self, net):
         self.net = net
@@ -693,9 +713,11 @@ class DBSREngine:
     def _pack(self, device):
         net = self.net
         stream = L.stream_ptr(device)
-        W = _Weights(self.dtype, device, stream)
+        # the DBSR convs' 16-bit weights by error-diffusion rounding (DBSREngine.WEIGHT_ROUNDING); PWC-Net's by
+        # round-to-nearest (diffusing them moved the fp16 prediction's error by nothing and the offsets' max error up)
+        W = _Weights(self.dtype, device, stream, rounding=DBSREngine.WEIGHT_ROUNDING)
         enc, mer, dec = net.encoder, net.merging, net.decoder
-        self.pwc = PWCPlanner(enc.alignment_net, W)
+        self.pwc = PWCPlanner(enc.alignment_net, _Weights(self.dtype, device, stream))
         self.enc_init = W.conv(enc.init_layer[0])
         self.enc_res = [(W.conv(b.conv1[0]), W.conv(b.conv2[0])) for b in enc.res_layers]
         self.enc_out = W.conv(enc.out_layer[0])
@@ -823,6 +845,10 @@ class DBSREngine:
         for k, (c1, c2) in enumerate(self.ofe_res):
             b, c = [j for j in range(3) if j != a]
             last = k == len(self.ofe_res) - 1
+            if DBSREngine.FUSED_RESBLOCK and plan.resblock(f'merge.ofe.res{k}', c1, c2, Fg, o[a], o[b],
+                                                           WP if last else o[c], hw, yc0=oc if last else 0):
+                a = c
+                continue
             plan.conv(f'merge.ofe.res{k}.conv1', c1, Fg, o[a], 0, hw, o[b], 0, L.ACT_RELU)
             if last:
                 plan.conv(f'merge.ofe.res{k}.conv2', c2, Fg, o[b], 0, hw, WP, oc, L.ACT_NONE, res=o[a],

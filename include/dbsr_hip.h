@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define DBSR_ABI_VERSION 18
+#define DBSR_ABI_VERSION 19
 
 enum { DBSR_F32 = 0, DBSR_BF16 = 1, DBSR_F16 = 2 };
 enum { DBSR_ACT_NONE = 0, DBSR_ACT_RELU = 1, DBSR_ACT_LRELU = 2 };      /* LeakyReLU slope 0.1 */
@@ -109,6 +109,15 @@ size_t dbsr_conv_packed_elems(int cout, int cin, int kh, int kw);
 int dbsr_conv_pack_weights(const float* w_f32, const float* bias_f32, int cout, int cin, int kh, int kw,
                            int dtype, int shuffle, void* w_packed, float* bias_out, void* stream);
 int dbsr_conv2d(const dbsr_conv_desc* d, void* stream);
+/* Error-diffusion rounding of conv weights to the 16-bit dtype (ABI 19; replaces the implicit round-to-nearest of
+ * the fp32 -> bf16/fp16 cast of the module's weights): w_out (fp32, torch layout [cout][cin][kh][kw], not aliasing
+ * w) = per output channel, its K = kh*kw*cin weights in packed K order (tap-major, then input channel) rounded in
+ * sequence with the running error carried, q_k = round(w_k - e_k), e_{k+1} = e_k + q_k - w_k.  Each value is
+ * exactly representable in dtype (so dbsr_conv_pack_weights keeps it); the carried error stays within half an ulp
+ * of the channel's largest weight, so each value is within one such ulp of w_k and the sum of a channel's errors
+ * within half of one.  cin*kh*kw <= 10368. */
+int dbsr_weights_round_diffuse(const float* w, int cout, int cin, int kh, int kw, int dtype, float* w_out,
+                               void* stream);
 /* Kernel selection for dbsr_conv2d (process-wide; for A/B testing): 2 (default) = pipelined
  * persistent 3x3 kernel for the large bf16 trunk convs (3x3/s1/p1/d1, cin > 16, width a multiple of
  * 48 or 64, height a multiple of 8, >= 256 tiles), else the two-barrier LDS-tiled 3x3 kernel where it
@@ -149,13 +158,15 @@ int dbsr_conv2d_head(const dbsr_conv_desc* d, const float* head_w, const float* 
  * NHWC slices aligned to 8 channels. */
 int dbsr_conv_shuffle_blur(const dbsr_conv_desc* d, const float* k9, void* stream);
 int dbsr_conv_shuffle_blur_ok(const dbsr_conv_desc* d);
-/* A whole 32-channel ResBlock in one launch (ABI 17; blocks.py:81-96, replaces the pair of dbsr_conv2d calls of
- * a decoder post-ResBlock, decoders.py:46-49): y = relu(x + conv2(relu(conv1(x)))).  c1 = conv1 as for dbsr_conv2d
+/* A whole ResBlock in one launch (ABI 17; blocks.py:81-96, replaces the pair of dbsr_conv2d calls of a decoder
+ * post-ResBlock, decoders.py:46-49, or -- 64 channels -- of a decoder pre-ResBlock, decoders.py:41-44): y = relu(x + conv2(relu(conv1(x)))).  c1 = conv1 as for dbsr_conv2d
  * (x -> its y, act ReLU), c2 = conv2 (its x, y, residual = c1's input, act none, post-act ReLU); c1->y and c2->x
  * name the intermediate, which this call neither reads nor writes (it stays on chip).  Bitwise equal to the two
- * calls.  Requires dbsr_resblock_ok(c1, c2): 16-bit 3x3/s1/p1 convs 32 -> 32, frames a multiple of 32 x 16,
- * NHWC slices aligned to 8 channels, and y not overlapping x (blocks read neighbouring tiles' halos of x while
- * others store y: an in-place call is refused with DBSR_E_ARG); c1->max_blocks caps the persistent grid. */
+ * calls.  Requires dbsr_resblock_ok(c1, c2): 16-bit 3x3/s1/p1 convs C -> C, C = 32 (frames a multiple of 32 x 16)
+ * or C = 64 (ABI 19; frames a multiple of 16 x 8, at most 2 tiles of 16 x 8 per CU -- the decoder's pre-ResBlocks;
+ * at the encoder's 2016 tiles the two weight-stationary launches measured faster), NHWC slices aligned to 8
+ * channels, and y not overlapping x (blocks read neighbouring tiles' halos of x while others store y: an in-place
+ * call is refused with DBSR_E_ARG); c1->max_blocks caps the persistent grid. */
 int dbsr_resblock(const dbsr_conv_desc* c1, const dbsr_conv_desc* c2, void* stream);
 int dbsr_resblock_ok(const dbsr_conv_desc* c1, const dbsr_conv_desc* c2);
 /* dbsr_resblock with the decoder's RGB predictor fused (ABI 18; decoders.py:59-61, the last post-ResBlock + the

@@ -105,6 +105,9 @@ def test_bench_shape_vs_oracle(synth_sd, bench_case, dtype):
     _check_bench(pred, aux['offsets'], bench_case, loose=dtype == torch.bfloat16)
     if dtype == torch.float16:
         assert rep['rms_clamped'] <= RMS_BAR, rep
+        # the margin under the bar: with the DBSR weights' error-diffusion rounding (DBSREngine.
+        # WEIGHT_ROUNDING, measured 3.19e-4; round-to-nearest 4.50e-4)
+        assert rep['rms_clamped'] <= 4.0e-4, rep
         assert rep['fw_rms'] <= 1e-3, rep
 
 

@@ -29,7 +29,7 @@ FAMILY = [('conv3x3_ws_kernel', 'conv3x3_ws'), ('conv3x3_pipe_kernel', 'conv3x3_
           ('conv3x3_tiled_kernel', 'conv3x3_tiled'), ('conv3x3_narrow_kernel', 'conv3x3_narrow'),
           ('conv1x1_kernel', 'conv1x1'),
           ('upsample_shuffle_kernel', 'conv1x1_shuffle'), ('upsample_blur_kernel', 'conv1x1_shuffle_blur'),
-          ('resblock32_kernel', 'resblock32'), ('conv_fuse_kernel', 'conv_fuse'), ('conv2d_kernel', 'conv2d_generic'),
+          ('resblock32_kernel', 'resblock32'), ('resblock64_kernel', 'resblock64'), ('conv_fuse_kernel', 'conv_fuse'), ('conv2d_kernel', 'conv2d_generic'),
           ('pwc_dense', 'pwc_dense'),
           ('pwc_extract_kernel', 'pwc_extract'), ('warp512_bf16_kernel', 'warp'), ('fuse512_bf16_kernel', 'fuse')]
 
