@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get('DBSR_HIP_LIB', os.path.join(_HERE, 'libdbsr_hip.so'))
 DBSR_F32, DBSR_BF16, DBSR_F16 = 0, 1, 2
 ACT_NONE, ACT_RELU, ACT_LRELU = 0, 1, 2
 OUT_NHWC, OUT_SHUFFLE, OUT_NCHW_F32 = 0, 1, 2
-ABI_VERSION = 19
+ABI_VERSION = 20
 
 
 class FrameMap(ctypes.Structure):
@@ -98,10 +98,14 @@ def lib():
                                            Tensor, c_void_p], c_int),
             'dbsr_backwarp': ([c_int, c_int, c_int, c_int, Tensor, Tensor, c_float, Tensor, c_void_p], c_int),
             'dbsr_warp_bilinear': ([c_int, c_int, c_int, c_int, Tensor, c_void_p, c_ll, Tensor, c_void_p], c_int),
+            'dbsr_fuse_relu_norm': ([c_int, c_int, c_int, c_int, Tensor, Tensor, Tensor, Tensor, Tensor, c_void_p], c_int),
+            'dbsr_burst_mean': ([c_int, c_int, c_int, c_int, Tensor, Tensor, c_void_p], c_int),
             'dbsr_fuse_softmax': ([c_int, c_int, c_int, c_int, Tensor, Tensor, Tensor, Tensor, Tensor, c_void_p],
                                   c_int),
             'dbsr_conv_fuse_softmax': ([ctypes.POINTER(ConvDesc), c_int, c_int, Tensor, Tensor, Tensor, Tensor,
                                         c_void_p], c_int),
+            'dbsr_conv_fuse_relu_norm': ([ctypes.POINTER(ConvDesc), c_int, c_int, Tensor, Tensor, Tensor, Tensor,
+                                          c_void_p], c_int),
             'dbsr_conv_fuse_ok': ([ctypes.POINTER(ConvDesc), c_int, c_int], c_int),
             'dbsr_fuse_partial': ([c_int, c_int, c_int, c_int, c_int, Tensor, Tensor, Tensor, c_void_p, c_void_p], c_int),
             'dbsr_fuse_combine': ([c_int, c_int, c_int, c_int, c_void_p, Tensor, c_void_p], c_int),
@@ -169,11 +173,11 @@ def lib():
 
 
 EXPORTED = ['dbsr_abi_version', 'dbsr_last_error', 'dbsr_conv_packed_elems', 'dbsr_conv_pack_weights',
-            'dbsr_weights_round_diffuse', 'dbsr_conv2d',
+            'dbsr_weights_round_diffuse', 'dbsr_fuse_relu_norm', 'dbsr_burst_mean', 'dbsr_conv2d',
             'dbsr_set_conv_algo', 'dbsr_conv_kernel_for', 'dbsr_conv_dispatch_variant', 'dbsr_conv_lane_reach', 'dbsr_conv_workspace_bytes', 'dbsr_conv2d_head',
             'dbsr_conv_head_ok', 'dbsr_conv_shuffle_blur', 'dbsr_conv_shuffle_blur_ok', 'dbsr_resblock', 'dbsr_resblock_ok', 'dbsr_resblock_head',
             'dbsr_correlation', 'dbsr_correlation_backward', 'dbsr_backwarp', 'dbsr_warp_bilinear', 'dbsr_fuse_softmax',
-            'dbsr_fuse_partial', 'dbsr_fuse_combine', 'dbsr_conv_fuse_softmax', 'dbsr_conv_fuse_ok',
+            'dbsr_fuse_partial', 'dbsr_fuse_combine', 'dbsr_conv_fuse_softmax', 'dbsr_conv_fuse_relu_norm', 'dbsr_conv_fuse_ok',
             'dbsr_conv_transpose_k4s2', 'dbsr_pack_burst', 'dbsr_flow_finalize', 'dbsr_gauss_blur3',
             'dbsr_merge_prep', 'dbsr_pwc_assemble', 'dbsr_zero', 'dbsr_nhwc_to_nchw_f32', 'dbsr_conv_wgrad_workspace_bytes', 'dbsr_conv_wgrad', 'dbsr_conv_wgrad_bias', 'dbsr_set_wgrad_algo', 'dbsr_head_forward', 'dbsr_head_backward_workspace_bytes', 'dbsr_head_backward',
             'dbsr_chan_sum_workspace_bytes', 'dbsr_chan_sum', 'dbsr_l1_loss_backward', 'dbsr_relu_grad', 'dbsr_unshuffle_gate',

@@ -3,6 +3,8 @@
 // Reference (models/dbsr/merging.py:55-57, 113-124):
 //   logits  = conv3x3(h) + bias  (last weight_predictor layer, 2*proj -> C, no activation)
 //   weights = softmax(logits.view(B, N, C, H, W), dim=1)          -> aux 'fusion_weights'
+//             (softmax=False, :119-121: relu(logits) / (sum_n relu(logits) + 1e-12); dbsr_conv_fuse_relu_norm,
+//              template flag RELU -- only the epilogue's normalisation differs)
 //   fused   = (all_feat * weights).sum(dim=1),  all_feat = [ref_feat, warped oth_feat]
 //
 // The two-kernel path (dbsr_conv2d to a logits buffer + dbsr_fuse_softmax) writes the logits [B*N, H, W, C]
@@ -99,7 +101,7 @@ struct FuseCfg {
     static_assert(LDS_U4 * 16 <= 160 * 1024, "weight ring + row ring + bias must fit the LDS");
 };
 
-template <typename T, int NF>
+template <typename T, int NF, bool RELU>
 __global__ __launch_bounds__(512, 1) void conv_fuse_kernel(FuseK k, int tiles_x, int tiles_y, int nct, int ntiles) {
     using C = FuseCfg<NF>;
     DBSR_OWN_SIMDS();
@@ -241,25 +243,39 @@ __global__ __launch_bounds__(512, 1) void conv_fuse_kernel(FuseK k, int tiles_x,
             });
         } else {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) m[e] = -INFINITY;
-#pragma unroll
-            for (int n = 0; n < NF; ++n)
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    const float l = acc[n][e >> 2][e & 3] + bv[e];      // the logit, fp32 (never rounded)
-                    acc[n][e >> 2][e & 3] = l;
-                    m[e] = fmaxf(m[e], l);
-                }
-#pragma unroll
             for (int e = 0; e < 8; ++e) sum[e] = 0.f;
+            if constexpr (RELU) {
+                // softmax=False (merging.py:119-121): relu(logit) / (sum over the burst + 1e-12)
 #pragma unroll
-            for (int n = 0; n < NF; ++n)
+                for (int n = 0; n < NF; ++n)
 #pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    const float x = __expf(acc[n][e >> 2][e & 3] - m[e]);
-                    acc[n][e >> 2][e & 3] = x;
-                    sum[e] += x;
-                }
+                    for (int e = 0; e < 8; ++e) {
+                        const float x = fmaxf(acc[n][e >> 2][e & 3] + bv[e], 0.f);   // fp32 logit, never rounded
+                        acc[n][e >> 2][e & 3] = x;
+                        sum[e] += x;
+                    }
+#pragma unroll
+                for (int e = 0; e < 8; ++e) sum[e] += 1e-12f;
+            } else {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) m[e] = -INFINITY;
+#pragma unroll
+                for (int n = 0; n < NF; ++n)
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        const float l = acc[n][e >> 2][e & 3] + bv[e];      // the logit, fp32 (never rounded)
+                        acc[n][e >> 2][e & 3] = l;
+                        m[e] = fmaxf(m[e], l);
+                    }
+#pragma unroll
+                for (int n = 0; n < NF; ++n)
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        const float x = __expf(acc[n][e >> 2][e & 3] - m[e]);
+                        acc[n][e >> 2][e & 3] = x;
+                        sum[e] += x;
+                    }
+            }
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
                 inv[e] = 1.0f / sum[e];
@@ -448,8 +464,10 @@ bool fuse_tensor_ok(const dbsr_tensor& t, int dt, int cout, int hw) {
 
 extern "C" int dbsr_conv_fuse_ok(const dbsr_conv_desc* d, int B, int N) { return fuse_conv_ok(d, B, N) ? 1 : 0; }
 
-extern "C" int dbsr_conv_fuse_softmax(const dbsr_conv_desc* d, int B, int N, dbsr_tensor ref, dbsr_tensor oth,
-                                      dbsr_tensor fused, dbsr_tensor weights, void* stream) {
+namespace {
+
+int conv_fuse(const dbsr_conv_desc* d, int B, int N, dbsr_tensor ref, dbsr_tensor oth, dbsr_tensor fused,
+              dbsr_tensor weights, bool relu, void* stream) {
     DBSR_CHECK_ARG(fuse_conv_ok(d, B, N), "conv_fuse_softmax: unsupported conv / burst (needs dbsr_conv_fuse_ok)");
     DBSR_CHECK_ARG(d->x.ptr && d->w, "conv_fuse_softmax: null pointer");
     const int C = d->cout, dt = d->x.dtype, hw = d->in_h * d->in_w;
@@ -511,12 +529,25 @@ extern "C" int dbsr_conv_fuse_softmax(const dbsr_conv_desc* d, int B, int N, dbs
     // block takes ~160 KB of LDS and its SIMDs, CUs meant for a concurrent lane); at least 8 (surplus blocks exit)
     grid = grid >= 8 ? grid / 8 * 8 : 8;
     hipStream_t s = (hipStream_t)stream;
+    auto launch = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(512), 0, s, k, tiles_x, tiles_y, nct, (int)nt);
+    };
     if (dt == DBSR_F16)
-        hipLaunchKernelGGL((conv_fuse_kernel<f16_t, FUSE_NF>), dim3(grid), dim3(512), 0, s, k, tiles_x, tiles_y, nct,
-                           (int)nt);
+        relu ? launch(conv_fuse_kernel<f16_t, FUSE_NF, true>) : launch(conv_fuse_kernel<f16_t, FUSE_NF, false>);
     else
-        hipLaunchKernelGGL((conv_fuse_kernel<bf16_t, FUSE_NF>), dim3(grid), dim3(512), 0, s, k, tiles_x, tiles_y, nct,
-                           (int)nt);
+        relu ? launch(conv_fuse_kernel<bf16_t, FUSE_NF, true>) : launch(conv_fuse_kernel<bf16_t, FUSE_NF, false>);
     DBSR_LAUNCH_CHECK();
     return 0;
+}
+
+}  // namespace
+
+extern "C" int dbsr_conv_fuse_softmax(const dbsr_conv_desc* d, int B, int N, dbsr_tensor ref, dbsr_tensor oth,
+                                      dbsr_tensor fused, dbsr_tensor weights, void* stream) {
+    return conv_fuse(d, B, N, ref, oth, fused, weights, false, stream);
+}
+
+extern "C" int dbsr_conv_fuse_relu_norm(const dbsr_conv_desc* d, int B, int N, dbsr_tensor ref, dbsr_tensor oth,
+                                        dbsr_tensor fused, dbsr_tensor weights, void* stream) {
+    return conv_fuse(d, B, N, ref, oth, fused, weights, true, stream);
 }

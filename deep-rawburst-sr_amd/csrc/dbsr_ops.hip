@@ -649,6 +649,73 @@ __global__ __launch_bounds__(256) void blur3_h16_kernel(int n, int h, int w, int
     }
 }
 
+// WeightedSum with softmax=False (merging.py:117-121): weights = relu(w) / (sum_n relu(w) + 1e-12), fused = sum_n
+// weights * feat -- two passes over the burst's logits (sum, then normalise and fuse), 4 channels per thread;
+// addressing as the softmax kernels
+template <typename T>
+__global__ __launch_bounds__(256) void fuse_relunorm_kernel(int B, int N, int hw, int groups, dbsr_tensor logits,
+                                                            dbsr_tensor ref, dbsr_tensor oth, dbsr_tensor fused,
+                                                            dbsr_tensor weights) {
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long long)B * hw * groups) return;
+    const int g = (int)(idx % groups);
+    const long long pix = idx / groups;
+    const int b = (int)(pix / hw), rr = (int)(pix - (long long)b * hw);
+    const int c = g * 4;
+    auto lg = [&](int n, float (&v)[4]) { Vec4<T>::ld(img_ptr<T>(logits, b * N + n) + (long long)rr * logits.ld + c, v); };
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int n = 0; n < N; ++n) {
+        float l[4];
+        lg(n, l);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s[j] += fmaxf(l[j], 0.f);
+    }
+    float den[4], acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) den[j] = s[j] + 1e-12f;
+    for (int n = 0; n < N; ++n) {
+        float l[4], fv[4], wn[4];
+        lg(n, l);
+        const T* fp = n == 0 ? img_ptr<T>(ref, b) + (long long)rr * ref.ld
+                             : img_ptr<T>(oth, b * (N - 1) + n - 1) + (long long)rr * oth.ld;
+        Vec4<T>::ld(fp + c, fv);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            wn[j] = fmaxf(l[j], 0.f) / den[j];
+            acc[j] = fmaf(fv[j], wn[j], acc[j]);
+        }
+        if (weights.ptr) {
+            if (weights.dtype == DBSR_F32)
+                Vec4<float>::st(img_ptr<float>(weights, b * N + n) + (long long)rr * weights.ld + c, wn);
+            else
+                Vec4<T>::st(img_ptr<T>(weights, b * N + n) + (long long)rr * weights.ld + c, wn);
+        }
+    }
+    Vec4<T>::st(img_ptr<T>(fused, b) + (long long)rr * fused.ld + c, acc);
+}
+
+// the burst mean of the projected embeddings (merging.py:81-82, use_base_frame=False): out[b] = (sum_n in[b*N+n]) / N
+template <typename T>
+__global__ __launch_bounds__(256) void burst_mean_kernel(int B, int N, int hw, int groups, dbsr_tensor in,
+                                                         dbsr_tensor out) {
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long long)B * hw * groups) return;
+    const int g = (int)(idx % groups);
+    const long long pix = idx / groups;
+    const int b = (int)(pix / hw), rr = (int)(pix - (long long)b * hw);
+    const int c = g * 4;
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int n = 0; n < N; ++n) {
+        float v[4];
+        Vec4<T>::ld(img_ptr<T>(in, b * N + n) + (long long)rr * in.ld + c, v);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a[j] += v[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) a[j] /= (float)N;
+    Vec4<T>::st(img_ptr<T>(out, b) + (long long)rr * out.ld + c, a);
+}
+
 inline unsigned nblocks(long long total, int bs) { return (unsigned)((total + bs - 1) / bs); }
 bool map_ok(const dbsr_tensor& t) { return t.ptr && t.map.fpg > 0; }
 bool vec_ok(const dbsr_tensor& t, int v) { return t.ld % v == 0 && t.c0 % v == 0; }
@@ -774,6 +841,41 @@ extern "C" int dbsr_fuse_partial(int B, int N, int hw, int c, int first_frame, d
         else
             hipLaunchKernelGGL((fuse_partial_kernel<T, 16>), dim3(nblocks(total, 256)), dim3(256), 0,
                                (hipStream_t)stream, B, N, hw, groups, first_frame, logits, ref, oth, stats);
+        DBSR_LAUNCH_CHECK();
+        return 0;
+    });
+}
+
+extern "C" int dbsr_fuse_relu_norm(int B, int N, int hw, int c, dbsr_tensor logits, dbsr_tensor ref, dbsr_tensor oth,
+                                   dbsr_tensor fused, dbsr_tensor weights, void* stream) {
+    DBSR_CHECK_ARG(map_ok(logits) && map_ok(ref) && map_ok(fused) && (N == 1 || map_ok(oth)), "fuse_relu_norm: bad tensor");
+    DBSR_CHECK_ARG(logits.dtype == ref.dtype && fused.dtype == ref.dtype && (N == 1 || oth.dtype == ref.dtype),
+                   "fuse_relu_norm: dtype mismatch");
+    DBSR_CHECK_ARG(B > 0 && N > 0 && hw > 0 && c % 4 == 0, "fuse_relu_norm: B, N, hw > 0 and c a multiple of 4");
+    DBSR_CHECK_ARG(vec_ok(logits, 4) && vec_ok(ref, 4) && vec_ok(fused, 4) && (N == 1 || vec_ok(oth, 4)),
+                   "fuse_relu_norm: ld/c0 must be multiples of 4");
+    if (weights.ptr) DBSR_CHECK_ARG(map_ok(weights) && vec_ok(weights, 4), "fuse_relu_norm: bad weights tensor");
+    const int groups = c / 4;
+    const long long total = (long long)B * hw * groups;
+    return by_dtype(ref.dtype, [&](auto* tag) {
+        using T = std::remove_pointer_t<decltype(tag)>;
+        hipLaunchKernelGGL(fuse_relunorm_kernel<T>, dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, B, N,
+                           hw, groups, logits, ref, oth, fused, weights);
+        DBSR_LAUNCH_CHECK();
+        return 0;
+    });
+}
+
+extern "C" int dbsr_burst_mean(int B, int N, int hw, int c, dbsr_tensor in, dbsr_tensor out, void* stream) {
+    DBSR_CHECK_ARG(map_ok(in) && map_ok(out) && in.dtype == out.dtype, "burst_mean: bad tensors");
+    DBSR_CHECK_ARG(B > 0 && N > 0 && hw > 0 && c % 4 == 0 && vec_ok(in, 4) && vec_ok(out, 4),
+                   "burst_mean: B, N, hw > 0, c and ld/c0 multiples of 4");
+    const int groups = c / 4;
+    const long long total = (long long)B * hw * groups;
+    return by_dtype(in.dtype, [&](auto* tag) {
+        using T = std::remove_pointer_t<decltype(tag)>;
+        hipLaunchKernelGGL(burst_mean_kernel<T>, dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, B, N, hw,
+                           groups, in, out);
         DBSR_LAUNCH_CHECK();
         return 0;
     });

@@ -328,8 +328,11 @@ __global__ void flow_finalize_kernel(int B, int N, int hf, int wf, dbsr_tensor f
         T* o = img_ptr<T>(om, f) + (long long)rr * om.ld;
 #pragma unroll
         for (int c = 0; c < 2; ++c) {     // torch.remainder: fmod, then shift into the divisor's sign
-            float m = fmodf(v[c], modulo);
-            if (m != 0.f && ((m < 0.f) != (modulo < 0.f))) m += modulo;
+            float m = v[c];
+            if (modulo != 0.f) {          // (0: offset_modulo None, merging.py:101-102 skips the remainder)
+                m = fmodf(v[c], modulo);
+                if (m != 0.f && ((m < 0.f) != (modulo < 0.f))) m += modulo;
+            }
             elem<T>::st(o + c, m);
         }
     }

@@ -152,9 +152,10 @@ def dbsrnet_cvpr2021(enc_init_dim, enc_num_res_blocks, enc_out_dim,
     load_state_dict of a full DBSR checkpoint, which carries them under encoder.alignment_net.*."""
     if activation != 'relu':
         raise NotImplementedError('only relu activation is on the hot path')
-    if not (use_offset and softmax and use_base_frame and offset_modulo == 1.0 and ref_offset_noise == 0.0):
-        raise NotImplementedError('hot path implements the dbsrnet_cvpr2021 defaults for use_offset/softmax/'
-                                  'use_base_frame/offset_modulo/ref_offset_noise (merging.py:79-121)')
+    # softmax, use_base_frame and offset_modulo take any value the reference accepts (the engine's variants,
+    # engine.merging_variant); use_offset=False and ref_offset_noise > 0 are refused there and here
+    if not use_offset or ref_offset_noise > 0.0:
+        raise NotImplementedError('hot path needs use_offset=True and ref_offset_noise=0 (merging.py:91-96)')
     alignment_net = PWCNet(load_pretrained=pwcnet_weights_path is not None, weights_path=pwcnet_weights_path)
     encoder = ResEncoderWarpAlignnet(enc_init_dim, enc_num_res_blocks, enc_out_dim, alignment_net,
                                      activation=activation, train_alignmentnet=train_alignmentnet)

@@ -70,6 +70,22 @@ def gauss_kernel3(sd, ksz=3):
     return [float(v) for v in K.reshape(-1)]
 
 
+def merging_variant(mer):
+    """The WeightedSum constructor flags the engine honours (merging.py:23-32, 79-121) as
+    (softmax, use_base_frame, offset_modulo for dbsr_flow_finalize: 0.0 = None, no remainder).
+    use_offset=False and ref_offset_noise > 0 (the latter draws torch.rand inside the forward) are refused."""
+    if not getattr(mer, 'use_offset', True):
+        raise NotImplementedError('WeightedSum(use_offset=False) is not on the HIP path (merging.py:91)')
+    if getattr(mer, 'ref_offset_noise', 0.0) > 0.0:
+        raise NotImplementedError('WeightedSum(ref_offset_noise > 0) is not on the HIP path: it draws random '
+                                  'reference offsets inside the forward (merging.py:92-96)')
+    m = getattr(mer, 'offset_modulo', None)
+    if m is not None and float(m) == 0.0:
+        raise ValueError('offset_modulo must be None or nonzero (x % 0 is NaN in the reference)')
+    return (bool(getattr(mer, 'softmax', True)), bool(getattr(mer, 'use_base_frame', False)),
+            0.0 if m is None else float(m))
+
+
 class NHWC:
     """Persistent buffer of n images of h x w pixels with ld elements per pixel."""
     def __init__(self, n, h, w, ld, dtype, device):
@@ -279,17 +295,19 @@ class Plan:
                                                                                       'conv2d_generic')
         return d
 
-    def conv_fuse(self, name, pc, B, N, x, in_hw, ref, oth, fused, weights, xmap=IDENTITY):
+    def conv_fuse(self, name, pc, B, N, x, in_hw, ref, oth, fused, weights, xmap=IDENTITY, softmax=True):
         """The weight predictor's last conv + softmax over the burst + fusion in one launch
-        (dbsr_conv_fuse_softmax: the logits never reach memory).  Returns the op index, or None when the
-        library does not serve the shape (the caller then emits the conv and dbsr_fuse_softmax)."""
+        (dbsr_conv_fuse_softmax: the logits never reach memory; softmax=False: dbsr_conv_fuse_relu_norm).  Returns
+        the op index, or None when the library does not serve the shape (the caller then emits the conv and
+        dbsr_fuse_softmax / dbsr_fuse_relu_norm)."""
         d = self._desc(name, pc, B * N, x, 0, in_hw, None, 0, L.ACT_NONE, xmap, IDENTITY, None, 0, IDENTITY,
                        L.ACT_NONE, L.OUT_NHWC, 0, L.NULL_TENSOR, None, False, None, 0, IDENTITY)
         if not L.lib().dbsr_conv_fuse_ok(ctypes.byref(d), B, N):
             return None
         H, W = in_hw
         flop = 2.0 * B * N * H * W * pc.cout * d.cin * pc.kh * pc.kw
-        self.add(name, L.lib().dbsr_conv_fuse_softmax, ctypes.byref(d), B, N, ref, oth, fused, weights,
+        fn = L.lib().dbsr_conv_fuse_softmax if softmax else L.lib().dbsr_conv_fuse_relu_norm
+        self.add(name, fn, ctypes.byref(d), B, N, ref, oth, fused, weights,
                  work=('flop', flop))
         self.kernel[len(self.ops) - 1] = 'conv_fuse'
         # hidden input + the N frames' features in + fusion weights out (when written) + fused out
@@ -687,8 +705,8 @@ class DBSREngine:
     # weight-predictor input conv split into a per-frame [proj, offfeat] conv + a per-burst base conv
     LINEAR_SPLIT = True
     # weight-predictor output conv + softmax + fusion in one kernel (dbsr_conv_fuse_softmax: the fp32 logits never
-    # reach memory) wherever the library serves the shape (16-bit, N = 14, cout % 128 == 0);
-    # otherwise dbsr_conv2d into a logits buffer + dbsr_fuse_softmax
+    # reach memory; softmax=False: dbsr_conv_fuse_relu_norm) wherever the library serves the shape
+    # (16-bit, N = 14, cout % 128 == 0); otherwise dbsr_conv2d into a logits buffer + dbsr_fuse_softmax / _relu_norm
     FUSED_WP_OUT = True
     # 16-bit weight rounding of the DBSR convs: 'diffuse' (dbsr_weights_round_diffuse: each output channel's rounding
     # errors carried along its K, their sum within half an ulp) or 'nearest'.  At configs[1] the fp16 prediction's
@@ -728,17 +746,25 @@ class DBSREngine:
         wp = list(mer.weight_predictor)
         self.wp_init = W.conv(wp[0][0])
         # linearity split of the first weight-predictor conv (merging.py:87-113): its input is
-        # [base, proj_f - base, offfeat_f] with base = proj of the burst's reference frame (use_base_frame), so
+        # [base, proj_f - base, offfeat_f] with base = proj of the burst's reference frame (use_base_frame) or the
+        # burst mean of the projections, so
         # conv(W)(input) = conv([W_diff | W_off])([proj_f, offfeat_f]) + conv(W_base - W_diff)(base): the second
         # term is one conv per burst instead of per frame, and the merge-prep copy of base / diff disappears
+        # constructor variants (merging.py:79-121): use_base_frame=False takes the burst mean of the projections as
+        # the base (dbsr_burst_mean, then the base conv: the split's algebra holds for any base); softmax=False
+        # normalises relu(logits) over the burst (dbsr_fuse_relu_norm); offset_modulo goes to flow_finalize
+        self.softmax, self.ref_base, self.offset_modulo = merging_variant(mer)
         pd = mer.feat_project_layer[0].out_channels
         self.wp_split = None
-        if DBSREngine.LINEAR_SPLIT and getattr(mer, 'use_base_frame', False) and pd % 32 == 0:
+        if DBSREngine.LINEAR_SPLIT and pd % 32 == 0:
             c0 = wp[0][0]
             geo = types.SimpleNamespace(stride=(1,), padding=c0.padding, dilation=c0.dilation)
             rest = lambda: (c0.weight.detach().float()[:, pd:], c0.bias)                               # noqa: E731
             base = lambda: (c0.weight.detach().float()[:, :pd] - c0.weight.detach().float()[:, pd:2 * pd], None)  # noqa: E731
             self.wp_split = (W.conv(geo, recipe=rest), W.conv(geo, recipe=base))
+        elif not self.ref_base:
+            raise NotImplementedError('use_base_frame=False runs on the linearity split: needs project_dim % 32 == 0 '
+                                      '(and DBSREngine.LINEAR_SPLIT)')
         self.wp_res = [(W.conv(b.conv1[0]), W.conv(b.conv2[0])) for b in wp[1:-1]]
         self.wp_out = W.conv(wp[-1][0])
         self.dec_init = W.conv(dec.init_layer[0])
@@ -818,7 +844,7 @@ class DBSREngine:
             self.pwc.build(plan, dt, dev, Fg, Hp, Wp, Pg, first_map=(N - 1, N, 0, 0), second_map=(N - 1, N, 1, 1),
                            rgb=sh['rgb'], flow_out=flow_out, rgb_map=fmap)
             plan.add('flow_finalize', lib.dbsr_flow_finalize, Bg, N, Hp // 4, Wp // 4, flow_out.d(0), H, W, Hp, Wp,
-                     sh['offsets'][off_p:].data_ptr(), 1.0, sh['om'].d(0, fmap))
+                     sh['offsets'][off_p:].data_ptr(), self.offset_modulo, sh['om'].d(0, fmap))
             plan.keep.append(flow_out)
         # (zero flow: offsets and om stay zero from initialisation)
         pd, od = self.proj.cout, self.ofe_init.cout
@@ -862,15 +888,33 @@ class DBSREngine:
     def _emit_base(self, plan, grp, N, H, W, sh, WP):
         """Linearity split: the reference frames' projection into WP[..., :pd] and the per-burst base conv
         (merging.py:77-89).  Needs only the encoder, so the first group's runs on lane 0 beside the
-        alignment chain; returns the base-term buffer BS."""
+        alignment chain; returns the base-term buffer BS (None with use_base_frame=False: the mean base needs
+        every frame's projection, _emit_mean_base)."""
         g0, g1 = grp
         Bg = g1 - g0
         rest, basec = self.wp_split
         plan.conv('merge.proj_ref', self.proj, Bg, sh['E'], 0, (H, W), WP, 0, L.ACT_RELU, xmap=(1, N, g0 * N, 1),
                   ymap=(1, N, 0, 1))
+        if not self.ref_base:
+            return None
         BS = NHWC(Bg, H, W, r8(basec.cout), self.dtype, self.device)
         plan.conv('merge.wp.base', basec, Bg, WP, 0, (H, W), BS, 0, L.ACT_NONE, xmap=(1, N, 0, 1))
         plan.keep.append(BS)
+        return BS
+
+    def _emit_mean_base(self, plan, grp, N, H, W, WP):
+        """use_base_frame=False (merging.py:81-82): the burst mean of all frames' projections WP[..., :pd]
+        (dbsr_burst_mean, fp32 sum) -> MB, then the per-burst base conv on it -> BS."""
+        g0, g1 = grp
+        Bg = g1 - g0
+        basec = self.wp_split[1]
+        pd = self.proj.cout
+        MB = NHWC(Bg, H, W, cpad(pd), self.dtype, self.device)
+        plan.add('merge.base_mean', L.lib().dbsr_burst_mean, Bg, N, H * W, pd, WP.d(0), MB.d(0),
+                 work=('byte', (N + 1.0) * Bg * H * W * pd * (4 if self.dtype == torch.float32 else 2)))
+        BS = NHWC(Bg, H, W, r8(basec.cout), self.dtype, self.device)
+        plan.conv('merge.wp.base', basec, Bg, MB, 0, (H, W), BS, 0, L.ACT_NONE)
+        plan.keep.extend([MB, BS])
         return BS
 
     def _emit_warp(self, plan, grp, N, H, W, sh, WP):
@@ -895,7 +939,8 @@ class DBSREngine:
     def _emit_merge(self, plan, grp, N, H, W, sh, WP, BS=None, Wf=None):
         """Warp (encoders.py:80) + projections, weight predictor (merging.py:61-113) of the group; returns
         the weight predictor's last hidden buffer and the warped embeddings Wf.  BS / Wf: the group's base
-        term / warped frames (with their projections) if _emit_base / _emit_warp already ran."""
+        term / warped frames (with their projections) if _emit_base / _emit_warp already ran (with the split,
+        _emit_base always has: BS None then means the mean base, computed here)."""
         dt, dev = self.dtype, self.device
         lib = L.lib()
         g0, g1 = grp
@@ -911,8 +956,8 @@ class DBSREngine:
             # the base term once per burst, added (broadcast over the burst's frames) as the residual of the
             # per-frame [proj, offfeat] conv before its ReLU
             rest = self.wp_split[0]
-            if BS is None:
-                BS = self._emit_base(plan, grp, N, H, W, sh, WP)
+            if BS is None:            # (use_base_frame=False: every frame's projection is in WP by now)
+                BS = self._emit_mean_base(plan, grp, N, H, W, WP)
             plan.conv('merge.wp.init', rest, Fg, WP, 0, hw, q[0], 0, L.ACT_NONE, res=BS, rmap=(N, 1, 0, 0),
                       post_act=L.ACT_RELU)
         else:
@@ -993,6 +1038,8 @@ class DBSREngine:
         plan.join(1)
         h, Wf = self._emit_merge(plan, grp, N, H, W, sh, WP, BS=BS, Wf=Wf)
         if mode == 'partial':
+            # (softmax=False and use_base_frame=False are refused by forward_partial: their statistics do not
+            # combine across frame shards with dbsr_fuse_combine's log-sum-exp)
             LG = self._emit_logits(plan, B * N, H, W, h)
             ST = torch.zeros(B, H, W, 3 * C, dtype=torch.float32, device=dev)
             plan.add('merge.fuse_partial', lib.dbsr_fuse_partial, B, N, H * W, C, first_frame, LG.d(0),
@@ -1001,14 +1048,17 @@ class DBSREngine:
         else:
             FUS = NHWC(B, H, W, C, dt, dev)
             feats = [E.d(0, (1, N, 0, 1)), Wf.d(0), FUS.d(0), FW.d(0)]
-            idx = plan.conv_fuse('merge.wp.out+fuse', self.wp_out, B, N, h, hw, *feats) \
+            idx = plan.conv_fuse('merge.wp.out+fuse', self.wp_out, B, N, h, hw, *feats, softmax=self.softmax) \
                 if DBSREngine.FUSED_WP_OUT else None
             if idx is not None:
                 plan.fuse_ops.append((idx, plan.ops[idx][1], FW.d(0), None))
             else:
                 LG = self._emit_logits(plan, B * N, H, W, h)
                 args = [B, N, H * W, C, LG.d(0)] + feats
-                plan.add('merge.fuse', lib.dbsr_fuse_softmax, *args)
+                if self.softmax:
+                    plan.add('merge.fuse', lib.dbsr_fuse_softmax, *args)
+                else:   # merging.py:119-121
+                    plan.add('merge.fuse_relu_norm', lib.dbsr_fuse_relu_norm, *args)
                 plan.fuse_ops.append((len(plan.ops) - 1, args, FW.d(0),
                                       ((2.0 * N + 1) * B * C * H * W * es, 1.0 * N * B * C * H * W * es)))
             self._decoder(plan, B, H, W, FUS, bufs, pred_out=bufs['pred'])
@@ -1219,6 +1269,10 @@ class DBSREngine:
         B, N, _, H, W = burst.shape
         if N < 2:
             raise ValueError('a frame shard needs the reference frame and at least one other frame')
+        if not (self.softmax and self.ref_base):
+            raise NotImplementedError('frame-sharded fusion needs softmax=True and use_base_frame=True: the '
+                                      'shards\' log-sum-exp statistics (dbsr_fuse_partial) combine only the softmax, '
+                                      'and a mean base needs every frame\'s projection')
         key = ('partial', B, N, H, W, int(first_frame))
         plan = self.plans.get(key)
         if plan is None:

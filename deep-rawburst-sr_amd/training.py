@@ -26,7 +26,7 @@ import torch.distributed as dist
 
 from . import _lib as L
 from ._lib import IDENTITY
-from .engine import NHWC, Plan, PWCPlanner, _Weights, cpad, gauss_kernel3, r8
+from .engine import NHWC, Plan, PWCPlanner, _Weights, cpad, gauss_kernel3, merging_variant, r8
 
 
 class _WS:
@@ -112,6 +112,12 @@ class DBSRTrainer:
             # flows, so refuse rather than train without alignment gradients
             raise NotImplementedError('DBSRTrainer: train_alignmentnet=True (PWC-Net training) is not on the HIP '
                                       'backward; build the net with train_alignmentnet=False (dbsrnet_cvpr2021 default)')
+        softmax, ref_base, self.offset_modulo = merging_variant(net.merging)
+        if not (softmax and ref_base):
+            # the backward kernels are the softmax's (dbsr_fuse_backward) and the reference-frame base's
+            # (dbsr_merge_prep_backward); the inference engine runs these variants, training does not
+            raise NotImplementedError('DBSRTrainer: WeightedSum(softmax=False / use_base_frame=False) is not on the '
+                                      'HIP backward (dbsrnet_cvpr2021 defaults: softmax=True, use_base_frame=True)')
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if (dist.is_available() and dist.is_initialized()) else 1
         # PWC-Net runs without gradients (train_alignmentnet=False: encoders.py:58-61); its parameters are left
@@ -238,7 +244,7 @@ class DBSRTrainer:
         self.pwc.build(plan, dt, dev, F, Hp, Wp, P, first_map=(N - 1, N, 0, 0), second_map=(N - 1, N, 1, 1), rgb=rgb,
                        flow_out=flow_out)
         plan.add('flow_finalize', lib.dbsr_flow_finalize, B, N, Hp // 4, Wp // 4, flow_out.d(0), H, W, Hp, Wp,
-                 offsets.data_ptr(), 1.0, om.d(0))
+                 offsets.data_ptr(), self.offset_modulo, om.d(0))
 
         def res_fwd(name, blocks, n, hw_, x, xc0, width, last_out=None):
             """ResBlocks with every activation kept: returns [(x, xc0, t, y, yc0)] per block."""

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define DBSR_ABI_VERSION 19
+#define DBSR_ABI_VERSION 20
 
 enum { DBSR_F32 = 0, DBSR_BF16 = 1, DBSR_F16 = 2 };
 enum { DBSR_ACT_NONE = 0, DBSR_ACT_RELU = 1, DBSR_ACT_LRELU = 2 };      /* LeakyReLU slope 0.1 */
@@ -212,6 +212,14 @@ int dbsr_warp_bilinear(int n, int h, int w, int c, dbsr_tensor feat, const float
 int dbsr_fuse_softmax(int B, int N, int hw, int c, dbsr_tensor logits, dbsr_tensor ref, dbsr_tensor oth,
                       dbsr_tensor fused, dbsr_tensor weights, void* stream);
 
+/* WeightedSum with softmax=False (ABI 20; merging.py:117-121): weights = relu(logits) / (sum over the burst of
+ * relu(logits) + 1e-12), fused = sum_n weights * features; arguments and addressing as dbsr_fuse_softmax. */
+int dbsr_fuse_relu_norm(int B, int N, int hw, int c, dbsr_tensor logits, dbsr_tensor ref, dbsr_tensor oth,
+                        dbsr_tensor fused, dbsr_tensor weights, void* stream);
+/* The burst mean of per-frame NHWC maps (ABI 20; merging.py:81-82, use_base_frame=False: the mean projected
+ * embedding as the base): out image b = (sum_n in image b*N+n) / N over c channels (fp32 sum, n in order). */
+int dbsr_burst_mean(int B, int N, int hw, int c, dbsr_tensor in, dbsr_tensor out, void* stream);
+
 /* The weight predictor's last conv fused with the softmax over the burst and the weighted sum
  * (models/dbsr/merging.py:55-57,113-124): logits = conv(d) + bias for the B*N frames
  * of d->x (frame b*N+n of burst b) never reach memory and are never rounded -- each (burst, 16x2 pixels,
@@ -224,6 +232,10 @@ int dbsr_fuse_softmax(int B, int N, int hw, int c, dbsr_tensor logits, dbsr_tens
  * multiples of 8 with c0 + cout <= ld (DBSR_E_ARG otherwise). */
 int dbsr_conv_fuse_softmax(const dbsr_conv_desc* d, int B, int N, dbsr_tensor ref, dbsr_tensor oth,
                            dbsr_tensor fused, dbsr_tensor weights, void* stream);
+/* As dbsr_conv_fuse_softmax with the ReLU normalisation of WeightedSum(softmax=False) (ABI 20; merging.py:119-121):
+ * weights = relu(logits) / (sum over the burst of relu(logits) + 1e-12), the fp32 logits never rounded. */
+int dbsr_conv_fuse_relu_norm(const dbsr_conv_desc* d, int B, int N, dbsr_tensor ref, dbsr_tensor oth,
+                             dbsr_tensor fused, dbsr_tensor weights, void* stream);
 int dbsr_conv_fuse_ok(const dbsr_conv_desc* d, int B, int N);
 
 /* Frame-sharded fusion (the softmax over the burst of models/dbsr/merging.py:116-124
@@ -249,7 +261,8 @@ int dbsr_pack_burst(int B, int N, int H, int W, const float* burst, dbsr_tensor 
 
 /* flow: NHWC fp32 2-ch slice [P][hf][wf] (P = B*(N-1) pairs).  offsets: fp32 NCHW [P][2][H][W] =
  * 20*bilinear(flow -> H x W) * (W/Wp, H/Hp).  offs_mod (optional): NHWC 2-ch slice, images b*N+n,
- * = offsets % modulo with zeros for n == 0 (merging.py:98-105). */
+ * = offsets % modulo (torch.remainder) with zeros for n == 0 (merging.py:98-105); modulo 0 = offset_modulo None
+ * (the offsets themselves). */
 int dbsr_flow_finalize(int B, int N, int hf, int wf, dbsr_tensor flow, int H, int W, int Hp, int Wp,
                        float* offsets, float modulo, dbsr_tensor offs_mod, void* stream);
 

@@ -245,20 +245,22 @@ def encoder(x, sd, kw, zero_flow=False):
 
 
 def merging(x, sd, kw, return_logits=False):
-    """WeightedSum.forward (merging.py:61-127) with use_offset=True, offset_modulo=1.0,
-    ref_offset_noise=0, softmax=True, use_base_frame=True (dbsrnet.py:47-53 defaults)."""
+    """WeightedSum.forward (merging.py:61-127) with use_offset=True and ref_offset_noise=0; offset_modulo (default 1.0,
+    None: no remainder, merging.py:101-102), softmax (default True; False: ReLU-normalised weights, :117-121) and
+    use_base_frame (default True; False: the mean projected embedding as the base, :79-82) from kw."""
     ref_feat = x['ref_feat'][:, :1].contiguous()
     oth_feat, offsets = x['oth_feat'], x['offsets']
     shape = ref_feat.shape
     all_feat = torch.cat((ref_feat, oth_feat), dim=1)
     proj = conv_block(all_feat.view(-1, *all_feat.shape[-3:]), sd, 'merging.feat_project_layer', ksz=1)
     proj = proj.view(*all_feat.shape[:2], -1, *all_feat.shape[-2:])
-    base = proj[:, :1].contiguous()
+    base = proj[:, :1].contiguous() if kw.get('use_base_frame', True) else proj.mean(dim=1, keepdim=True)
     diff = (proj - base).view(-1, *proj.shape[-3:])
     base = base.expand(-1, all_feat.shape[1], -1, -1, -1).contiguous().view(-1, *base.shape[-3:])
     offsets_base = offsets.new_zeros((shape[0], 1, 2, *shape[-2:]))
     offsets_all = torch.cat((offsets_base, offsets), dim=1).view(-1, 2, *shape[-2:])
-    offsets_all = offsets_all % 1.0
+    if kw.get('offset_modulo', 1.0) is not None:
+        offsets_all = offsets_all % kw.get('offset_modulo', 1.0)
     of = conv_block(offsets_all, sd, 'merging.offset_feat_extractor.0')
     for i in range(1, 1 + kw.get('num_offset_feat_extractor_res', 1)):
         of = res_block(of, sd, f'merging.offset_feat_extractor.{i}')
@@ -271,7 +273,11 @@ def merging(x, sd, kw, return_logits=False):
     w = w.view(shape[0], -1, *w.shape[-3:])
     if return_logits:
         return all_feat, w
-    wn = F.softmax(w, dim=1)
+    if kw.get('softmax', True):
+        wn = F.softmax(w, dim=1)
+    else:
+        wn = F.relu(w)
+        wn = wn / (wn.sum(dim=1, keepdim=True) + 1e-12)
     fused = (all_feat * wn).sum(dim=1)
     return {'fused_enc': fused, 'fusion_weights': wn}
 

@@ -409,3 +409,22 @@ def test_resblock_rejects_output_aliasing_input(L):
     c1, c2 = _rb_pair(L, x, x)
     assert lib.dbsr_resblock(ctypes.byref(c1), ctypes.byref(c2), None) == -1                 # DBSR_E_ARG
     assert b'overlap' in lib.dbsr_last_error()
+
+
+def test_constructor_variants_accepted_and_refused():
+    """dbsrnet_cvpr2021 takes the reference's WeightedSum flags softmax / use_base_frame / offset_modulo (the engine
+    runs them: engine.merging_variant) and refuses use_offset=False and ref_offset_noise > 0 (merging.py:91-96)."""
+    import dbsr_amd
+    from dbsr_amd.engine import merging_variant
+    kw = dict(enc_init_dim=8, enc_num_res_blocks=1, enc_out_dim=16, dec_init_conv_dim=8, dec_num_pre_res_blocks=1,
+              dec_post_conv_dim=32, dec_num_post_res_blocks=1, offset_feat_dim=8, weight_pred_proj_dim=32)
+    assert merging_variant(dbsr_amd.dbsrnet_cvpr2021(**kw).merging) == (True, True, 1.0)
+    net = dbsr_amd.dbsrnet_cvpr2021(**kw, softmax=False, use_base_frame=False, offset_modulo=None)
+    assert merging_variant(net.merging) == (False, False, 0.0)
+    assert merging_variant(dbsr_amd.dbsrnet_cvpr2021(**kw, offset_modulo=0.5).merging) == (True, True, 0.5)
+    with pytest.raises(NotImplementedError, match='use_offset'):
+        dbsr_amd.dbsrnet_cvpr2021(**kw, use_offset=False)
+    with pytest.raises(NotImplementedError, match='ref_offset_noise'):
+        dbsr_amd.dbsrnet_cvpr2021(**kw, ref_offset_noise=0.1)
+    with pytest.raises(ValueError, match='offset_modulo'):
+        merging_variant(dbsr_amd.dbsrnet_cvpr2021(**kw, offset_modulo=0.0).merging)

@@ -212,3 +212,85 @@ def test_fusion_weights_reference_contract(synth_sd):
     s = fw.sum(dim=1)
     assert float((s - 1).abs().max()) <= 5e-3            # 16-bit stored weights, fp32 softmax
     assert set(aux.keys()) == {'offsets', 'fusion_weights'} and aux.get('fusion_weights') is fw
+
+
+VARIANTS = {'relu': dict(softmax=False), 'mean': dict(use_base_frame=False), 'nomod': dict(offset_modulo=None),
+            'all': dict(softmax=False, use_base_frame=False, offset_modulo=None)}
+
+
+def _variant_net(synth_sd, case, dtype=torch.float32):
+    import dbsr_amd
+    net = dbsr_amd.dbsrnet_cvpr2021(**dict(dbsr_amd.DBSR_SYNTHETIC_KWARGS, **VARIANTS[case]))
+    net.load_state_dict(synth_sd)
+    net = net.to(DEV).eval()
+    net.set_compute_dtype(dtype)
+    return net
+
+
+@pytest.mark.parametrize('case', list(VARIANTS))
+def test_e2e_constructor_variants_fp32(golden, synth_sd, case):
+    """WeightedSum(softmax=False / use_base_frame=False / offset_modulo=None) through the engine (dbsr_fuse_relu_norm,
+    dbsr_burst_mean + the split's base conv, flow_finalize without remainder) against the reference network built
+    with the same flags (tests/golden/make_golden_variants.py); fp32 at the north_star's 1e-3."""
+    g = golden('variants')
+    net = _variant_net(synth_sd, case)
+    with torch.no_grad():
+        pred, aux = net(torch.from_numpy(g['e2e_burst']).to(DEV))
+    pred = pred.cpu()
+    np.testing.assert_allclose(aux['offsets'].cpu().numpy(), g['e2e_offsets'], atol=1e-3, rtol=0)
+    np.testing.assert_allclose(pred[..., 100:164, 100:164].numpy(), g[f'e2e_{case}_pred_crop'], atol=1e-3, rtol=0)
+    fw = aux['fusion_weights'].cpu()
+    np.testing.assert_allclose(fw[:, :, :16, 8:16, 8:16].numpy(), g[f'e2e_{case}_fw_crop'], atol=1e-3, rtol=0)
+    np.testing.assert_allclose(fw.double().sum(dim=(-2, -1)).numpy(), g[f'e2e_{case}_fw_sum'], rtol=1e-3, atol=0.5)
+    np.testing.assert_allclose(pred.double().sum(dim=(-2, -1)).numpy(), g[f'e2e_{case}_pred_sum'], rtol=1e-4)
+    names = [op[2] for op in net._get_engine().plans[(1, 4, 48, 48)].ops]
+    assert ('merge.fuse_relu_norm' in names) == (not VARIANTS[case].get('softmax', True))
+    assert ('merge.base_mean' in names) == (not VARIANTS[case].get('use_base_frame', True))
+
+
+@pytest.mark.parametrize('case', ['mean_nomod', 'all', 'all_n14'])
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
+def test_e2e_variants_16bit_vs_oracle(synth_sd, dtype, case):
+    """The variant flags in 16-bit compute, B=2 N=6, against the fp32 oracle with the same flags.  With the softmax
+    (use_base_frame=False, offset_modulo=None) the prediction keeps the 16-bit forward's usual max-abs bound (2e-2).
+    With softmax=False the reference's weights relu(l) / sum relu(l) jump wherever a logit crosses 0 next to a
+    near-zero burst sum (merging.py:119-121), so 16-bit logit rounding moves single pixels by up to ~0.1: there the
+    bound is on the RMS (fp16 1e-2, bf16 2e-2; measured at B=2 N=6: bf16 1.18e-2), and the ReLU-normalised weights
+    must sum to 1 (or 0 where every logit is <= 0).  all_n14: B=1 N=14 48x48, where the weight predictor's last conv
+    runs fused with the ReLU normalisation (dbsr_conv_fuse_relu_norm, fp32 logits)."""
+    import dbsr_amd
+    from dbsr_amd.burst import synthetic_bursts
+    from oracle import dbsr_oracle as orc
+    flags = VARIANTS['all'] if case.startswith('all') else dict(use_base_frame=False, offset_modulo=None)
+    shape = (1, 14, 48, 48) if case == 'all_n14' else (2, 6, 40, 40)
+    burst, _ = synthetic_bursts(*shape, sr_factor=8, seed=31)
+    net = dbsr_amd.dbsrnet_cvpr2021(**dict(dbsr_amd.DBSR_SYNTHETIC_KWARGS, **flags))
+    net.load_state_dict(synth_sd)
+    net = net.to(DEV).eval().set_compute_dtype(dtype)
+    with torch.no_grad():
+        pred, aux = net(burst.to(DEV))
+    ref, raux = orc.dbsr_forward(burst, synth_sd, kw=dict(dbsr_amd.DBSR_SYNTHETIC_KWARGS, **flags))
+    err = (pred.float().cpu() - ref).abs()
+    rms = float(err.pow(2).mean().sqrt())
+    print(dtype, case, 'variants max-abs', float(err.max()), 'rms', rms)
+    names = [op[2] for op in net._get_engine().plans[shape].ops]
+    assert ('merge.wp.out+fuse' in names) == (case == 'all_n14')
+    if case.startswith('all'):
+        assert rms <= (1e-2 if dtype == torch.float16 else 2e-2)
+        s = aux['fusion_weights'].sum(dim=1)
+        assert float(torch.minimum((s - 1).abs(), s.abs()).max()) <= 1e-2
+    else:       # (bf16: test_gpu_parity's element bound PRED_Q_MAX, 800 of 2^14 quanta)
+        assert float(err.max()) <= (2e-2 if dtype == torch.float16 else 800 / 2 ** 14)
+
+
+def test_variants_refused_where_unsupported(golden, synth_sd):
+    """Frame-sharded fusion and training refuse softmax=False / use_base_frame=False (their statistics and
+    backward kernels are the softmax's and the reference-frame base's)."""
+    from dbsr_amd.training import DBSRTrainer
+    g = golden('variants')
+    for case in ('relu', 'mean'):
+        net = _variant_net(synth_sd, case)
+        with pytest.raises(NotImplementedError, match='frame-sharded'):
+            net._get_engine().forward_partial(torch.from_numpy(g['e2e_burst']).to(DEV), 1)
+        with pytest.raises(NotImplementedError, match='softmax=False'):
+            DBSRTrainer(net.set_compute_dtype(torch.float32))

@@ -19,8 +19,9 @@ DEV = 'cuda'
 pytestmark = pytest.mark.gpu
 
 
-def _case(B, N, H, W, cin, C, dt, seed, want_fw=True, strided=False):
-    """strided: every tensor addressed through a non-identity frame map -- the hidden input as every
+def _case(B, N, H, W, cin, C, dt, seed, want_fw=True, strided=False, relu=False):
+    """relu: WeightedSum(softmax=False) -- dbsr_conv_fuse_relu_norm / dbsr_fuse_relu_norm, torch relu(l) / (sum + 1e-12).
+    strided: every tensor addressed through a non-identity frame map -- the hidden input as every
     second stored image (f -> 2f + 1), the reference embeddings behind one leading burst (b -> (b + 1) N), the
     warped frames behind 3 images, the fused output behind one image; the kernel derives all of its addressing
     from these maps (affine_frames)."""
@@ -54,12 +55,13 @@ def _case(B, N, H, W, cin, C, dt, seed, want_fw=True, strided=False):
         feats = [E.d(0, (1, N, eo, 1)), Wf.d(0, (1, 1, wo, 1)), FUS.d(0, (1, 1, fo, 1)),
                  FW.d(0) if want_fw else L.NULL_TENSOR]
         if fused_path:
-            idx = plan.conv_fuse('fz', pc, B, N, X, (H, W), *feats, xmap=xmap)
+            idx = plan.conv_fuse('fz', pc, B, N, X, (H, W), *feats, xmap=xmap, softmax=not relu)
             assert idx is not None, 'dbsr_conv_fuse_ok rejected the case'
         else:
             LG = NHWC(B * N, H, W, C, dt, dev)
             plan.conv('lg', pc, B * N, X, 0, (H, W), LG, 0, L.ACT_NONE, xmap=xmap)
-            plan.add('fuse', L.lib().dbsr_fuse_softmax, B, N, H * W, C, LG.d(0), *feats)
+            fn = L.lib().dbsr_fuse_relu_norm if relu else L.lib().dbsr_fuse_softmax
+            plan.add('fuse', fn, B, N, H * W, C, LG.d(0), *feats)
         plan.finalize_workspace(dev)
         plan.run(s)
         torch.cuda.synchronize()
@@ -70,7 +72,11 @@ def _case(B, N, H, W, cin, C, dt, seed, want_fw=True, strided=False):
     hb = h.to(dt).float()
     wb = w_cpu.to(dt).float()
     lg = F.conv2d(hb, wb, b_cpu, padding=1).reshape(B, N, C, H, W)
-    wts = torch.softmax(lg, dim=1)
+    if relu:
+        wts = F.relu(lg)
+        wts = wts / (wts.sum(dim=1, keepdim=True) + 1e-12)
+    else:
+        wts = torch.softmax(lg, dim=1)
     fz = (feat.to(dt).float() * wts).sum(dim=1)
     ref = (fz.permute(0, 2, 3, 1), wts.reshape(B * N, C, H, W).permute(0, 2, 3, 1))
     return outs, ref
@@ -162,3 +168,29 @@ def test_engine_fused_wp_out_matches_default(synth_sd, dt):
     dq = ((p1 - p0).abs() * 2 ** 14).flatten()
     assert torch.quantile(dq[:2 ** 24].float(), 0.999) <= 320 and dq.max() <= 800, (dq.max().item(),)
     np.testing.assert_allclose(w1.numpy(), w0.numpy(), atol=2e-3, rtol=5e-2 if dt == torch.bfloat16 else 1e-2)
+
+
+def _frac_outside(a, b, atol, rtol):
+    return float(((a - b).abs() > atol + rtol * b.abs()).float().mean())
+
+
+@pytest.mark.parametrize('dt', [torch.float16, torch.bfloat16])
+def test_conv_fuse_relu_norm(dt):
+    """softmax=False (merging.py:119-121) at the bench shape's layer: the fused kernel (fp32 logits) against torch on
+    the same operands and against the two-kernel path (16-bit logits + dbsr_fuse_relu_norm).  relu(l) / sum relu(l)
+    has no floor under its denominator: where a pixel's positive logits sum to ~1e-4 a 1e-6 change of a logit (K
+    order) moves its weights by ~1e-2, so the bounds are the softmax test's tolerances met by all but 1e-4 of the
+    elements against torch (1e-3 against the rounded-logit path)."""
+    B, N, H, W, cin, C = 2, 14, 48, 48, 128, 512
+    outs, (rf, rw) = _case(B, N, H, W, cin, C, dt, seed=901, relu=True)
+    (f1, w1), (f0, w0) = outs[True], outs[False]
+    eps = 2.0 ** -8 if dt == torch.bfloat16 else 2.0 ** -11
+    assert _frac_outside(w1, rw, 1e-3, 2 * eps) <= 1e-4
+    assert _frac_outside(f1, rf, 1e-2, 4 * eps) <= 1e-4
+    rt = 5e-2 if dt == torch.bfloat16 else 1e-2
+    assert _frac_outside(w1, w0, 2e-3, rt) <= 1e-3
+    assert _frac_outside(f1, f0, 8e-2 if dt == torch.bfloat16 else 2e-2, rt) <= 1e-3
+    assert (w1 - rw).abs().mean() <= (w0 - rw).abs().mean()
+    s = w1.reshape(B, N, H, W, C).sum(dim=1)
+    assert float(torch.minimum((s - 1).abs(), s.abs()).max()) < 0.05     # 1, or 0 where every logit is <= 0
+    assert float((s == 0).float().mean()) > 0                               # (both cases occur here)

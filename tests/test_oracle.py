@@ -59,3 +59,38 @@ def test_oracle_pixshuffle_blur(golden):
     shp = out.shape
     out = F.conv2d(out.reshape(-1, 1, *shp[-2:]), K, padding=1).view(shp)
     np.testing.assert_allclose(out.numpy(), g['up_out'], atol=1e-6, rtol=0)
+
+
+# ---------------- WeightedSum constructor variants (tests/golden/make_golden_variants.py) ----------------
+VARIANTS = {'relu': dict(softmax=False), 'mean': dict(use_base_frame=False), 'nomod': dict(offset_modulo=None),
+            'all': dict(softmax=False, use_base_frame=False, offset_modulo=None)}
+
+
+@pytest.mark.parametrize('case', list(VARIANTS))
+def test_oracle_merging_variants(golden, case):
+    """oracle.merging with softmax / use_base_frame / offset_modulo against the reference WeightedSum module
+    (merging.py:61-127) on offsets reaching past [-3, 3)."""
+    g = golden('variants')
+    sd = {'merging.' + k[len('merging_sd.'):]: torch.from_numpy(g[k]) for k in g if k.startswith('merging_sd.')}
+    kw = {**dict(num_weight_predictor_res=1, num_offset_feat_extractor_res=1, offset_modulo=1.0, use_base_frame=True),
+          **VARIANTS[case]}
+    x = {'ref_feat': torch.from_numpy(g['merging_ref_feat']), 'oth_feat': torch.from_numpy(g['merging_oth_feat']),
+         'offsets': torch.from_numpy(g['merging_offsets'])}
+    with torch.no_grad():
+        r = orc.merging(x, sd, kw)
+    np.testing.assert_allclose(r['fused_enc'].numpy(), g[f'merging_{case}_fused'], atol=1e-6, rtol=0)
+    np.testing.assert_allclose(r['fusion_weights'].numpy(), g[f'merging_{case}_weights'], atol=1e-6, rtol=0)
+
+
+@pytest.mark.parametrize('case', ['relu', 'all'])
+def test_oracle_e2e_variants(golden, synth_sd, case):
+    """The whole oracle forward with the variant flags against the reference dbsrnet_cvpr2021 built with them."""
+    g = golden('variants')
+    kw = dict(orc.DBSR_SYNTHETIC_KWARGS, **VARIANTS[case])
+    with torch.no_grad():
+        pred, aux = orc.dbsr_forward(torch.from_numpy(g['e2e_burst']), synth_sd, kw=kw)
+    np.testing.assert_allclose(aux['offsets'].numpy(), g['e2e_offsets'], atol=1e-5, rtol=0)
+    np.testing.assert_allclose(pred[..., 100:164, 100:164].numpy(), g[f'e2e_{case}_pred_crop'], atol=1e-5, rtol=0)
+    fw = aux['fusion_weights']
+    np.testing.assert_allclose(fw[:, :, :16, 8:16, 8:16].numpy(), g[f'e2e_{case}_fw_crop'], atol=1e-6, rtol=0)
+    np.testing.assert_allclose(pred.double().sum(dim=(-2, -1)).float().numpy(), g[f'e2e_{case}_pred_sum'], rtol=1e-5)
