@@ -98,6 +98,8 @@ def lib():
                                            Tensor, c_void_p], c_int),
             'dbsr_backwarp': ([c_int, c_int, c_int, c_int, Tensor, Tensor, c_float, Tensor, c_void_p], c_int),
             'dbsr_warp_bilinear': ([c_int, c_int, c_int, c_int, Tensor, c_void_p, c_ll, Tensor, c_void_p], c_int),
+            'dbsr_warp_project': ([c_int, c_int, c_int, c_int, Tensor, c_void_p, c_ll, Tensor, c_void_p, c_void_p, c_int,
+                                   Tensor, c_void_p], c_int),
             'dbsr_fuse_relu_norm': ([c_int, c_int, c_int, c_int, Tensor, Tensor, Tensor, Tensor, Tensor, c_void_p], c_int),
             'dbsr_burst_mean': ([c_int, c_int, c_int, c_int, Tensor, Tensor, c_void_p], c_int),
             'dbsr_fuse_softmax': ([c_int, c_int, c_int, c_int, Tensor, Tensor, Tensor, Tensor, Tensor, c_void_p],
@@ -176,7 +178,7 @@ EXPORTED = ['dbsr_abi_version', 'dbsr_last_error', 'dbsr_conv_packed_elems', 'db
             'dbsr_weights_round_diffuse', 'dbsr_fuse_relu_norm', 'dbsr_burst_mean', 'dbsr_conv2d',
             'dbsr_set_conv_algo', 'dbsr_conv_kernel_for', 'dbsr_conv_dispatch_variant', 'dbsr_conv_lane_reach', 'dbsr_conv_workspace_bytes', 'dbsr_conv2d_head',
             'dbsr_conv_head_ok', 'dbsr_conv_shuffle_blur', 'dbsr_conv_shuffle_blur_ok', 'dbsr_resblock', 'dbsr_resblock_ok', 'dbsr_resblock_head',
-            'dbsr_correlation', 'dbsr_correlation_backward', 'dbsr_backwarp', 'dbsr_warp_bilinear', 'dbsr_fuse_softmax',
+            'dbsr_correlation', 'dbsr_correlation_backward', 'dbsr_backwarp', 'dbsr_warp_bilinear', 'dbsr_warp_project', 'dbsr_fuse_softmax',
             'dbsr_fuse_partial', 'dbsr_fuse_combine', 'dbsr_conv_fuse_softmax', 'dbsr_conv_fuse_relu_norm', 'dbsr_conv_fuse_ok',
             'dbsr_conv_transpose_k4s2', 'dbsr_pack_burst', 'dbsr_flow_finalize', 'dbsr_gauss_blur3',
             'dbsr_merge_prep', 'dbsr_pwc_assemble', 'dbsr_zero', 'dbsr_nhwc_to_nchw_f32', 'dbsr_conv_wgrad_workspace_bytes', 'dbsr_conv_wgrad', 'dbsr_conv_wgrad_bias', 'dbsr_set_wgrad_algo', 'dbsr_head_forward', 'dbsr_head_backward_workspace_bytes', 'dbsr_head_backward',

@@ -224,6 +224,7 @@ class Plan:
         self.streams = {}
         self.max_blocks = 0  # CU cap for lane-0 persistent convs issued while a side lane runs
         self.max_blocks_cap = 0
+        self.early_names, self.early_cap = (), 0   # lane-0 convs capped at early_cap instead (DBSREngine.LANE0_EARLY_*)
         self.plan_rows = None  # (slab rows, whole-image rows): convs dispatch as on the whole image (plan_h)
 
     def add(self, name, fn, *args, work=None):
@@ -386,7 +387,8 @@ class Plan:
         d.out_mode, d.shuffle = out_mode, shuffle
         d.workspace, d.workspace_bytes = None, 0
         d.precise = 1 if precise else 0
-        d.max_blocks = self.max_blocks if self.lane == 0 else 0
+        d.max_blocks = (self.early_cap if name in self.early_names and self.max_blocks else self.max_blocks) \
+            if self.lane == 0 else 0
         if self.plan_rows is not None:
             slab, full = self.plan_rows
             if oh % slab == 0:
@@ -694,6 +696,10 @@ class PWCPlanner:
 # ==================================================================================================
 class DBSREngine:
     LANE0_CU_SHARE = 0.5      # CU share of lane 0's persistent convs while the PWC lane runs (tools/capbench.sh)
+    # the first LANE0_EARLY_CONVS encoder convs (enc.init, enc.res0.conv1, ...) at CU share LANE0_EARLY_SHARE instead:
+    # PWC-Net's coarse levels (1x1 .. 8x8 pixels per pair) leave most of the chip idle while they run
+    LANE0_EARLY_CONVS = 0
+    LANE0_EARLY_SHARE = 0.5
     # bf16: fuse the RGB predictor into the last decoder ResBlock conv (False: separate fp32 kernel)
     FUSED_HEAD = True
     # PixelShuffle upsampler conv + shuffle + blur in one kernel (dbsr_conv_shuffle_blur)
@@ -702,6 +708,10 @@ class DBSREngine:
     # the encoder's, the offset-feature extractor's and the decoder's 64-channel pre blocks)
     FUSED_RESBLOCK = True
     FUSED_RESBLOCK64 = True   # (A/B switch for the 64-channel kernel alone)
+    # the warp of the other frames + their feature projection in one launch (dbsr_warp_project; 16-bit, 512 channels,
+    # with the linearity split, whose projections go straight into the weight-predictor input).  Off: measured slower
+    # than the two launches it replaces at the bench shape (230 vs 186 us, tools/bench_wp.py)
+    FUSED_WARP_PROJ = False
     # weight-predictor input conv split into a per-frame [proj, offfeat] conv + a per-burst base conv
     LINEAR_SPLIT = True
     # weight-predictor output conv + softmax + fusion in one kernel (dbsr_conv_fuse_softmax: the fp32 logits never
@@ -928,11 +938,25 @@ class DBSREngine:
         Wf = NHWC(max(Pg, 1), H, W, C, dt, dev)
         es = 4 if dt == torch.float32 else 2
         if Pg > 0:
-            plan.add('warp', L.lib().dbsr_warp_bilinear, Pg, H, W, C, E.d(0, (N - 1, N, 1 + off_f, 1)),
-                     sh['offsets'][off_p:].data_ptr(), 2 * H * W, Wf.d(0),
-                     work=('byte', 2.0 * Pg * C * H * W * es + 8.0 * Pg * H * W))
-            if self.wp_split is not None:
-                plan.conv('merge.proj_oth', self.proj, Pg, Wf, 0, (H, W), WP, 0, L.ACT_RELU, ymap=(N - 1, N, 1, 1))
+            pd = self.proj.cout
+            fused = (self.wp_split is not None and DBSREngine.FUSED_WARP_PROJ and dt != torch.float32 and C == 512
+                     and pd % 16 == 0 and pd <= 64 and self.proj.kh == 1 and self.proj.cin == C)
+            if fused:
+                # warp + the projection of the warped frames in one launch (the 512-channel warped frames are not
+                # read back from HBM); the op stays in the warp family, its bytes + the projection's output
+                plan.add('warp+proj', L.lib().dbsr_warp_project, Pg, H, W, C, E.d(0, (N - 1, N, 1 + off_f, 1)),
+                         sh['offsets'][off_p:].data_ptr(), 2 * H * W, Wf.d(0), self.proj.w.data_ptr(),
+                         self.proj.bias.data_ptr() if self.proj.bias is not None else None, pd,
+                         WP.d(0, (N - 1, N, 1, 1)),
+                         work=('byte', 2.0 * Pg * C * H * W * es + 8.0 * Pg * H * W + 1.0 * Pg * pd * H * W * es))
+                plan.kernel[len(plan.ops) - 1] = 'warp'
+            else:
+                plan.add('warp', L.lib().dbsr_warp_bilinear, Pg, H, W, C, E.d(0, (N - 1, N, 1 + off_f, 1)),
+                         sh['offsets'][off_p:].data_ptr(), 2 * H * W, Wf.d(0),
+                         work=('byte', 2.0 * Pg * C * H * W * es + 8.0 * Pg * H * W))
+                if self.wp_split is not None:
+                    plan.conv('merge.proj_oth', self.proj, Pg, Wf, 0, (H, W), WP, 0, L.ACT_RELU,
+                              ymap=(N - 1, N, 1, 1))
         plan.keep.append(Wf)
         return Wf
 
@@ -1012,6 +1036,11 @@ class DBSREngine:
         WP = self._emit_flow(plan, grp, N, H, W, sh)          # PWC-Net on lane 1
         plan.switch(0)
         plan.max_blocks = plan.max_blocks_cap = plan_cap
+        if plan_cap and DBSREngine.LANE0_EARLY_CONVS:
+            names = ['enc.init'] + [f'enc.res{i}.conv{j}' for i in range(len(self.enc_res)) for j in (1, 2)]
+            plan.early_names = set(names[:DBSREngine.LANE0_EARLY_CONVS])
+            plan.early_cap = int(torch.cuda.get_device_properties(dev).multi_processor_count *
+                                 DBSREngine.LANE0_EARLY_SHARE)
         # ---------------- encoder (encoders.py:66-72), whole batch ----------------
         e = [NHWC(F, H, W, r8(self.enc_init.cout), dt, dev) for _ in range(3)]
         plan.conv('enc.init', self.enc_init, F, raw, 0, hw, e[0], 0, L.ACT_RELU)

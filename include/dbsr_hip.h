@@ -205,6 +205,15 @@ int dbsr_backwarp(int n, int h, int w, int c, dbsr_tensor in, dbsr_tensor flow, 
  * [n][2][h][w] (the `offsets` tensor), flow_img_stride elements per image. */
 int dbsr_warp_bilinear(int n, int h, int w, int c, dbsr_tensor feat, const float* flow,
                        long long flow_img_stride, dbsr_tensor out, void* stream);
+/* dbsr_warp_bilinear fused with the 1x1 feature projection of the warped frames (ABI 20; encoders.py:80 then
+ * merging.py:34-36,75 on the warped embeddings): out = warp(feat) exactly as dbsr_warp_bilinear stores it, and
+ * proj_out = ReLU(proj_w . out + proj_b) computed from those stored 16-bit values (fp32 accumulation; equal to
+ * dbsr_conv2d of the 1x1 conv on `out` up to the K summation order).  c == 512, 16-bit feat / out / proj_out of one
+ * dtype; proj_w = the 1x1 conv's weights packed by dbsr_conv_pack_weights (cin 512), proj_b fp32 or NULL,
+ * proj_cout 16 / 32 / 48 / 64; proj_out image f of the n warped frames, channels [c0, c0 + proj_cout). */
+int dbsr_warp_project(int n, int h, int w, int c, dbsr_tensor feat, const float* flow, long long flow_img_stride,
+                      dbsr_tensor out, const void* proj_w, const float* proj_b, int proj_cout, dbsr_tensor proj_out,
+                      void* stream);
 
 /* Softmax over the burst of logits[b,n] and weighted sum of feats[b,n].  Frame (b,n): logits image
  * b*N+n; feature image: n==0 -> ref (map applied to b), n>0 -> oth (map applied to b*(N-1)+n-1).

@@ -10,7 +10,7 @@ mode=${2:-full}
 out=gpurun_out/$tag
 mkdir -p $out
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests/test_gpu_e2e.py tests/test_gpu_resblock.py tests/test_gpu_fuse.py tests/test_gpu_weight_round.py \
+timeout -k 10 400 python -u -m pytest tests/test_gpu_warp_proj.py tests/test_gpu_e2e.py tests/test_gpu_resblock.py tests/test_gpu_fuse.py tests/test_gpu_weight_round.py \
     tests/test_gpu_ops.py -x -v --timeout 200 --timeout-method thread > $out/pytest_new.log 2>&1 \
     || { echo "new tests failed rc=$?"; grep -E "FAIL|Error|assert" $out/pytest_new.log | head; tail -3 $out/pytest_new.log; exit 1; }
 tail -1 $out/pytest_new.log
