@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get('DBSR_HIP_LIB', os.path.join(_HERE, 'libdbsr_hip.so'))
 DBSR_F32, DBSR_BF16, DBSR_F16 = 0, 1, 2
 ACT_NONE, ACT_RELU, ACT_LRELU = 0, 1, 2
 OUT_NHWC, OUT_SHUFFLE, OUT_NCHW_F32 = 0, 1, 2
-ABI_VERSION = 20
+ABI_VERSION = 21
 
 
 class FrameMap(ctypes.Structure):

@@ -1589,6 +1589,28 @@ int launch_ws(const ConvK& k, const dbsr_conv_desc* d, int px, hipStream_t s) {
     return 0;
 }
 
+int g_ks128_enabled = 1;
+// the K-split weight-stationary 128-channel kernel (conv128.hip) serves `d`: 16-bit 3x3/s1/p1/d1, 96 < cin <= 128,
+// cout == 128, aligned NHWC output / residual, no gate, frames a multiple of 16 x 8, the whole image (no plan_h slab)
+// and at least 128 tiles (the weight predictor's input conv and ResBlocks, merging.py:86-90, 98-101)
+bool use_ks128(const dbsr_conv_desc* d) {
+    if (!g_ks128_enabled || !is16(d->x.dtype) || d->precise || d->kh != 3 || d->kw != 3 || d->stride != 1 ||
+        d->pad != 1 || d->dil != 1 || cin_pad(d->cin) != 128 || d->cout != 128 || d->out_mode != DBSR_OUT_NHWC ||
+        d->y.dtype != d->x.dtype || d->gate.ptr)
+        return false;
+    if (d->y.ld % 8 || d->y.c0 % 8 || (d->res.ptr && (d->res.ld % 8 || d->res.c0 % 8))) return false;
+    if (d->out_w % ks128::TW || d->out_h % ks128::TH || (d->plan_h > 0 && d->plan_h != d->out_h)) return false;
+    if ((long long)d->in_h * d->in_w * d->x.ld * 2 >= (1LL << 31)) return false;   // 32-bit buffer offsets per frame
+    return (long long)d->n_frames * (d->out_w / ks128::TW) * (d->out_h / ks128::TH) >= 128;
+}
+int launch_ks128(const ConvK& k, const dbsr_conv_desc* d, hipStream_t s) {
+    int epi = 0;                        // the pipelined kernel's compile-time epilogues 1-3, run-time 0 otherwise
+    if (!k.r && k.act == DBSR_ACT_RELU) epi = 1;
+    else if (k.r && k.act == DBSR_ACT_NONE && k.post_act == DBSR_ACT_RELU) epi = 2;
+    else if (!k.r && k.act == DBSR_ACT_NONE) epi = 3;
+    return ks128_launch(k, d->n_frames, d->x.dtype == DBSR_F16, epi, k.max_blocks, num_cus(), s);
+}
+
 // ------------------------------------------------------------------------------------------------
 // Fused 32-channel ResBlock (blocks.py:81-96: y = relu(x + conv2(relu(conv1(x)))), 3x3/s1/p1 convs with bias):
 // the decoder's 384x384 post-ResBlocks (decoders.py:46-49).  The two ws32 launches it replaces move 377 MB per
@@ -2083,6 +2105,7 @@ int dispatch_conv(const ConvK& k, const dbsr_conv_desc* d, const dbsr_conv_desc*
         const int px = pick_ws(sel, d);
         if (px < 0) return slab_misfit(d, sel);
         if (px) return dispatch_ws<T>(px, k, d, sel, s);
+        if (use_ks128(sel)) return launch_ks128(k, d, s);
         const int cfg = pick_pipe(sel);
         if (cfg && !pipe_fits(cfg, d)) return slab_misfit(d, sel);
         if (cfg) return dispatch_pipe<T>(cfg, k, d, s);
@@ -2668,6 +2691,7 @@ int kernel_for(const dbsr_conv_desc* d) {
     if (use_pointwise(sel)) return 5;
     if (is16(d->x.dtype)) {
         if (pick_ws(sel)) return 4;
+        if (use_ks128(sel)) return 7;
         if (pick_pipe(sel)) return 2;
         if (use_narrow(sel)) return 6;
     }
@@ -2722,6 +2746,8 @@ extern "C" int dbsr_conv_dispatch_variant(const dbsr_conv_desc* d) {
         var = np >= 512 * 256 ? 4 : np >= 512 * 128 ? 2 : 1;
     } else if (kf == 4) {
         var = ws_narrow(sel) ? 6408 : ws_short(sel) ? 1608 : 1616;
+    } else if (kf == 7) {
+        var = ks128::TW * 100 + ks128::TH;
     } else if (kf == 2) {
         var = pick_pipe(sel);
     } else if (kf == 1) {
@@ -2756,11 +2782,13 @@ extern "C" size_t dbsr_conv_workspace_bytes(const dbsr_conv_desc* d) {
 }
 
 extern "C" int dbsr_set_conv_algo(int algo) {
-    DBSR_CHECK_ARG(algo >= 0 && algo <= 4, "set_conv_algo: 0 generic, 1 two-barrier tiled, 2 weight-stationary + "
-                   "pipelined + tiled (default), 3 pipelined wherever the shape allows, 4 as 2 without weight-stationary");
+    DBSR_CHECK_ARG(algo >= 0 && algo <= 5, "set_conv_algo: 0 generic, 1 two-barrier tiled, 2 weight-stationary + "
+                   "K-split 128-channel + pipelined + tiled (default), 3 pipelined wherever the shape allows, 4 as 2 "
+                   "without the weight-stationary kernels, 5 as 2 without the K-split 128-channel kernel");
     g_tiled_enabled = algo >= 1;
     g_pipe_enabled = algo == 3 ? 2 : algo >= 2 ? 1 : 0;
-    g_ws_enabled = algo == 2;
+    g_ws_enabled = algo == 2 || algo == 5;
+    g_ks128_enabled = algo == 2;
     g_narrow_enabled = algo >= 2;
     return 0;
 }

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define DBSR_ABI_VERSION 20
+#define DBSR_ABI_VERSION 21
 
 enum { DBSR_F32 = 0, DBSR_BF16 = 1, DBSR_F16 = 2 };
 enum { DBSR_ACT_NONE = 0, DBSR_ACT_RELU = 1, DBSR_ACT_LRELU = 2 };      /* LeakyReLU slope 0.1 */
@@ -123,12 +123,17 @@ int dbsr_weights_round_diffuse(const float* w, int cout, int cin, int kh, int kw
  * 48 or 64, height a multiple of 8, >= 256 tiles), else the two-barrier LDS-tiled 3x3 kernel where it
  * applies (3x3, stride 1, pad == dilation in {1,2,4,8}, cin > 16, out >= 8x8, NHWC out), else the
  * generic implicit-GEMM kernel; 1 = no pipelined kernel; 0 = generic kernel only; 3 = as 2 but the
- * pipelined kernel at any tile count (tests); 4 = as 2 without the weight-stationary kernels. */
+ * pipelined kernel at any tile count (tests); 4 = as 2 without the weight-stationary kernels (both the Cin <= 64
+ * one and the K-split 128-channel one); 5 = as 2 without the K-split 128-channel kernel (ABI 21).  Under 2 the
+ * 16-bit 128 -> 128 3x3/s1/p1 convs of >= 128 tiles of 16 x 8 pixels (merging.py:86-90, 98-101: the weight
+ * predictor's input conv and ResBlocks) run on the K-split weight-stationary kernel (kernel_for 7), which sums
+ * each output as (input channels 0-63) + (64-127) in fp32, not in the pipelined kernel's order. */
 int dbsr_set_conv_algo(int algo);
 /* Which kernel dbsr_conv2d would launch for `d` under the current selection: 5 pointwise projection
  * (16-bit 1x1, cin 32..512 a power of two, cout 32 | 64, no residual: merging.py:34), 4 weight-stationary,
  * 3 PixelShuffle upsampler (bf16 1x1 with DBSR_OUT_SHUFFLE, 32 channels per sub-pixel), 2 pipelined,
- * 6 narrow-output 3x3 (16-bit, cout <= 4, cin >= 256, pad 1: the PWC level-2 flow head), 1 LDS-tiled, 0 generic. */
+ * 6 narrow-output 3x3 (16-bit, cout <= 4, cin >= 256, pad 1: the PWC level-2 flow head), 7 K-split
+ * weight-stationary 128 -> 128 3x3 (ABI 21), 1 LDS-tiled, 0 generic. */
 int dbsr_conv_kernel_for(const dbsr_conv_desc* d);
 /* The full dispatch decision for `d`: kernel_for * 1000000 + the variant (weight-stationary: tile width*100 +
  * height; pipelined: tile config; LDS-tiled: cout tile*1000 + pixel tile; generic: cout tile*10000 + pixel
