@@ -57,16 +57,17 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ks128_kernel(ConvK k, int tile
     const int kh = wave >> 2, q = wave & 3;
     const int H = k.in_h, W = k.in_w;
     // epilogues (the pipelined kernel's): 1 bias + ReLU, 2 bias + residual then ReLU, 3 bias, 0 run-time act /
-    // residual / post-act
-    const bool has_res = EPI == 2 || (EPI == 0 && k.r != nullptr);
+    // residual / post-act, 5 as 0 then the training dgrad's ReLU-backward gate (out *= gate > 0)
+    constexpr bool RT = EPI == 0 || EPI == 5, has_gate = EPI == 5;
+    const bool has_res = EPI == 2 || (RT && k.r != nullptr);
     auto act1 = [&](float v) {
         if constexpr (EPI == 1) return fmaxf(v, 0.f);
-        else if constexpr (EPI == 0) return apply_act(v, k.act);
+        else if constexpr (RT) return apply_act(v, k.act);
         else return v;
     };
     auto act2 = [&](float v) {
         if constexpr (EPI == 2) return fmaxf(v, 0.f);
-        else if constexpr (EPI == 0) return apply_act(v, k.post_act);
+        else if constexpr (RT) return apply_act(v, k.post_act);
         else return v;
     };
 
@@ -84,7 +85,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ks128_kernel(ConvK k, int tile
     }
     if (threadIdx.x < 128) lbias[threadIdx.x] = k.bias ? k.bias[threadIdx.x] : 0.f;   // (cout == 128) ordered by the
                                                                                       // loop's first barrier
-    struct Tile { const T* xf; long long y_off, r_off; int y0, x0; };
+    struct Tile { const T* xf; long long y_off, r_off, g_off; int y0, x0; };
     auto decode = [&](int i) {
         const int t = rb_tile(i, blockIdx.x, gridDim.x, ntiles);
         const int tx = t % tiles_x, r = t / tiles_x, ty = r % tiles_y, f = r / tiles_y;
@@ -94,6 +95,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ks128_kernel(ConvK k, int tile
         const long long pix = (long long)tl.y0 * k.out_w + tl.x0;
         tl.y_off = map_frame(k.ym, f) * k.y_is + k.y_c0 + pix * k.y_ld;
         tl.r_off = has_res ? map_frame(k.rm, f) * k.r_is + k.r_c0 + pix * k.r_ld : 0;
+        tl.g_off = has_gate ? map_frame(k.gm, f) * k.g_is + k.g_c0 + pix * k.g_ld : 0;
         return tl;
     };
     const int my_tiles = ntiles / (int)gridDim.x + ((int)blockIdx.x < ntiles % (int)gridDim.x ? 1 : 0);
@@ -201,13 +203,15 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ks128_kernel(ConvK k, int tile
                     xch[((wave * HALF + NB * b + j) * 2 + h) * 64 + ln] = __builtin_bit_cast(u32x4_t, acc[j][h]);
         });
         // ---- this wave's own groups: residual loads, k-steps ----
+        // (run-time epilogues: loaded in the epilogue beside the gate, which leaves the k-steps their registers)
         u32x4_t resv[HALF];
-        if (has_res) {
+        auto load_res = [&]() {
 #pragma unroll
             for (int j = 0; j < HALF; ++j)
                 resv[j] = *(const u32x4_t*)((const T*)k.r + cur.r_off + ((long long)(own0 + j) * k.out_w + col) * k.r_ld +
                                             32 * q + 8 * g);
-        }
+        };
+        if (!RT && has_res) load_res();
         f32x4_t mine[HALF][2];
         StaticFor<0, HALF / NB>::run([&](auto b_) {
             constexpr int b = decltype(b_)::value;
@@ -228,6 +232,14 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ks128_kernel(ConvK k, int tile
         const int partner = wave ^ 4;
         const float4 b0 = *(const float4*)(lbias + 32 * q + 8 * g), b1 = *(const float4*)(lbias + 32 * q + 8 * g + 4);
         const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+        if (RT && has_res) load_res();
+        u32x4_t gatev[has_gate ? HALF : 1];     // EPI 5: the gate, all pieces in flight at once
+        if constexpr (has_gate) {
+#pragma unroll
+            for (int j = 0; j < HALF; ++j)
+                gatev[j] = *(const u32x4_t*)((const T*)k.gt + cur.g_off + ((long long)(own0 + j) * k.out_w + col) * k.g_ld +
+                                             32 * q + 8 * g);
+        }
 #pragma unroll
         for (int j = 0; j < HALF; ++j) {
             const f32x4_t o0 = __builtin_bit_cast(f32x4_t, xch[((partner * HALF + j) * 2 + 0) * 64 + ln]);
@@ -243,6 +255,13 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ks128_kernel(ConvK k, int tile
                 for (int e = 0; e < 4; ++e) {
                     v[2 * e] = act2(v[2 * e] + H16<T>::lo(resv[j][e]));
                     v[2 * e + 1] = act2(v[2 * e + 1] + H16<T>::hi(resv[j][e]));
+                }
+            }
+            if constexpr (has_gate) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    v[2 * e] = H16<T>::lo(gatev[j][e]) > 0.f ? v[2 * e] : 0.f;
+                    v[2 * e + 1] = H16<T>::hi(gatev[j][e]) > 0.f ? v[2 * e + 1] : 0.f;
                 }
             }
             u32x4_t o;
@@ -271,6 +290,7 @@ int ks128_launch(const ConvK& k, int n_frames, bool f16, int epi, int max_blocks
         case 1: DBSR_KS_LAUNCH(TT, 1); break;    \
         case 2: DBSR_KS_LAUNCH(TT, 2); break;    \
         case 3: DBSR_KS_LAUNCH(TT, 3); break;    \
+        case 5: DBSR_KS_LAUNCH(TT, 5); break;    \
         default: DBSR_KS_LAUNCH(TT, 0); break;   \
     }
     if (f16) {

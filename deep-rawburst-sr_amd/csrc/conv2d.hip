@@ -1591,21 +1591,24 @@ int launch_ws(const ConvK& k, const dbsr_conv_desc* d, int px, hipStream_t s) {
 
 int g_ks128_enabled = 1;
 // the K-split weight-stationary 128-channel kernel (conv128.hip) serves `d`: 16-bit 3x3/s1/p1/d1, 96 < cin <= 128,
-// cout == 128, aligned NHWC output / residual, no gate, frames a multiple of 16 x 8, the whole image (no plan_h slab)
-// and at least 128 tiles (the weight predictor's input conv and ResBlocks, merging.py:86-90, 98-101)
+// cout == 128, aligned NHWC output / residual / gate, frames a multiple of 16 x 8, the whole image (no plan_h slab)
+// and at least 128 tiles (the weight predictor's input conv and ResBlocks, merging.py:86-90, 98-101, and their
+// gated dgrads in the training step)
 bool use_ks128(const dbsr_conv_desc* d) {
     if (!g_ks128_enabled || !is16(d->x.dtype) || d->precise || d->kh != 3 || d->kw != 3 || d->stride != 1 ||
         d->pad != 1 || d->dil != 1 || cin_pad(d->cin) != 128 || d->cout != 128 || d->out_mode != DBSR_OUT_NHWC ||
-        d->y.dtype != d->x.dtype || d->gate.ptr)
+        d->y.dtype != d->x.dtype)
         return false;
     if (d->y.ld % 8 || d->y.c0 % 8 || (d->res.ptr && (d->res.ld % 8 || d->res.c0 % 8))) return false;
+    if (d->gate.ptr && (d->gate.ld % 8 || d->gate.c0 % 8 || d->gate.dtype != d->y.dtype)) return false;
     if (d->out_w % ks128::TW || d->out_h % ks128::TH || (d->plan_h > 0 && d->plan_h != d->out_h)) return false;
     if ((long long)d->in_h * d->in_w * d->x.ld * 2 >= (1LL << 31)) return false;   // 32-bit buffer offsets per frame
     return (long long)d->n_frames * (d->out_w / ks128::TW) * (d->out_h / ks128::TH) >= 128;
 }
 int launch_ks128(const ConvK& k, const dbsr_conv_desc* d, hipStream_t s) {
-    int epi = 0;                        // the pipelined kernel's compile-time epilogues 1-3, run-time 0 otherwise
-    if (!k.r && k.act == DBSR_ACT_RELU) epi = 1;
+    int epi = 0;                        // the pipelined kernel's compile-time epilogues 1-3, run-time 0 otherwise,
+    if (k.gt) epi = 5;                  // 5 with the gate
+    else if (!k.r && k.act == DBSR_ACT_RELU) epi = 1;
     else if (k.r && k.act == DBSR_ACT_NONE && k.post_act == DBSR_ACT_RELU) epi = 2;
     else if (!k.r && k.act == DBSR_ACT_NONE) epi = 3;
     return ks128_launch(k, d->n_frames, d->x.dtype == DBSR_F16, epi, k.max_blocks, num_cus(), s);

@@ -129,7 +129,7 @@ constexpr int TW = 16, TH = 8;                                // output tile (fr
 }  // namespace rb64
 
 // launch of the K-split weight-stationary 128 -> 128 conv (conv128.hip); epi: the pipelined kernel's epilogue codes
-// 0-3 (0 run-time act / residual / post-act, 1 bias + ReLU, 2 bias + residual then ReLU, 3 bias)
+// (0 run-time act / residual / post-act, 1 bias + ReLU, 2 bias + residual then ReLU, 3 bias, 5 as 0 + the gate)
 int ks128_launch(const ConvK& k, int n_frames, bool f16, int epi, int max_blocks, int cus, hipStream_t s);
 namespace ks128 {
 constexpr int TW = 16, TH = 8;                                // output tile (frames must be multiples)

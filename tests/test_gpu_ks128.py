@@ -65,9 +65,41 @@ def test_ks128_vs_torch_and_pipe(dt, shape, epi):
     assert (outs[2] == outs[5]).float().mean() > 0.9
 
 
+@pytest.mark.parametrize('dt', [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize('use_res', [False, True])
+def test_ks128_gated_dgrad_epilogue(dt, use_res):
+    """Epilogue 5, the training step's gated dgrads of the weight predictor's ResBlocks (training.py res_bwd):
+    dX = conv_input_grad(dY) [+ residual], times (gate > 0), no bias, at the training shape's frame size."""
+    from dbsr_amd import _lib, ops
+    N, H, W = 3, 128, 128
+    gen = torch.Generator().manual_seed(11 + use_res)
+    dy = torch.randn(N, 128, H, W, generator=gen)
+    w = torch.randn(128, 128, 3, 3, generator=gen) / (128 * 9) ** 0.5
+    res = torch.randn(N, 128, H, W, generator=gen) if use_res else None
+    gate = torch.randn(N, 128, H, W, generator=gen)
+    dyr, wr, gr = dy.to(dt).float(), w.to(dt).float(), gate.to(dt).float()
+    ref = torch.nn.grad.conv2d_input((N, 128, H, W), wr, dyr, padding=1)
+    if use_res:
+        ref = ref + res.to(dt).float()
+    ref = ref * (gr > 0)
+    outs = {}
+    try:
+        for algo in (2, 5):
+            _lib.lib().dbsr_set_conv_algo(algo)
+            outs[algo] = ops.conv2d_dgrad(dy.to(DEV), w.to(DEV), residual=res.to(DEV) if use_res else None,
+                                          gate=gate.to(DEV), compute_dtype=dt).float().cpu()
+            assert (ops.conv2d_dgrad.last_kernel == 7) == (algo == 2)
+    finally:
+        _lib.lib().dbsr_set_conv_algo(2)
+    ulp = 2.0 ** (-10 if dt == torch.float16 else -7)
+    np.testing.assert_allclose(outs[2].numpy(), ref.numpy(), atol=4 * ulp, rtol=2 * ulp)
+    np.testing.assert_allclose(outs[2].numpy(), outs[5].numpy(), atol=4 * ulp, rtol=2 * ulp)
+    assert ((outs[2] == 0) | (gr > 0)).all()
+
+
 def test_ks128_not_picked_off_shape():
     """Shapes outside the kernel's contract go elsewhere: cout != 128, a frame width not a multiple of 16, too
-    few tiles, a gate (training dgrad)."""
+    few tiles, cin 64."""
     from dbsr_amd import ops
     for (N, cin, H, W, cout) in [(16, 128, 32, 64, 96), (16, 128, 32, 56, 128), (2, 128, 48, 48, 128),
                                  (16, 64, 32, 64, 128)]:
