@@ -37,7 +37,13 @@ constexpr int PIECES = NCH * CPX / 16;                        // 46 1-KiB halo p
 constexpr int BUF_U4 = NCH * CH_U4;                           // one halo buffer (47,104 B)
 constexpr int NW = 8;
 constexpr int PER = (PIECES + NW - 1) / NW;                   // DMA pieces per wave per tile
-constexpr int NB = 2;                                         // 16-pixel groups per MFMA batch
+#ifndef DBSR_KS_NB                                            // (experiment builds: tools/build_variant.sh)
+#define DBSR_KS_NB 2
+#endif
+#ifndef DBSR_KS_ABL                                           // timing-only ablations: 1 no k-steps, 2 no halo DMA
+#define DBSR_KS_ABL 0                                         // after the first tile, 4 no partial-sum exchange
+#endif
+constexpr int NB = DBSR_KS_NB;                                // 16-pixel groups per MFMA batch
 constexpr int HALF = TH / 2;                                  // groups a wave finishes (4)
 constexpr int XCH_U4 = NW * HALF * 2 * 64;                    // exchange: [wave][group][16-cout block][lane]
 constexpr int LDS_U4 = 2 * BUF_U4 + XCH_U4;
@@ -128,6 +134,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ks128_kernel(ConvK k, int tile
     // runs after k-step st's MFMAs (the DMA pieces of the next tile)
     auto taps = [&](int buf, auto j0_, f32x4_t (&acc)[NB][2], auto&& hook) {
         constexpr int J0 = decltype(j0_)::value, NS = 18;
+        if constexpr ((DBSR_KS_ABL & 1) != 0) {
+            for (int j = 0; j < NB; ++j) acc[j][0] = acc[j][1] = f32x4_t{(float)(J0 + j + buf), 0.f, 0.f, 0.f};
+            StaticFor<0, NS>::run([&](auto s_) { hook(decltype(s_)::value); });
+            return;
+        }
         const int g = lane >> 4, col = lane & 15;
         const unsigned base = lds0 + (unsigned)((buf * BUF_U4 + kh * 2 * CH_U4) * 16);
         unsigned ba[8];                 // byte address of pixel col + rho, k-group g (halo_phys), rho = imm & 7
@@ -186,7 +197,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ks128_kernel(ConvK k, int tile
             constexpr int b = decltype(b_)::value;
             f32x4_t acc[NB][2];
             auto hook = [&](int st) {
-                if constexpr (b == 0) {
+                if constexpr (b == 0 && (DBSR_KS_ABL & 2) == 0) {     // (ablation 2: stale halos after tile 0)
                     if (more) {
 #pragma unroll
                         for (int it = 0; it < PER; ++it)
@@ -200,7 +211,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ks128_kernel(ConvK k, int tile
             for (int j = 0; j < NB; ++j)
 #pragma unroll
                 for (int h = 0; h < 2; ++h)
-                    xch[((wave * HALF + NB * b + j) * 2 + h) * 64 + ln] = __builtin_bit_cast(u32x4_t, acc[j][h]);
+                    if constexpr ((DBSR_KS_ABL & 4) == 0)
+                        xch[((wave * HALF + NB * b + j) * 2 + h) * 64 + ln] = __builtin_bit_cast(u32x4_t, acc[j][h]);
+                    else if (acc[j][h][0] == 12345.f) xch[ln] = u32x4_t{0u, 0u, 0u, 0u};
         });
         // ---- this wave's own groups: residual loads, k-steps ----
         // (run-time epilogues: loaded in the epilogue beside the gate, which leaves the k-steps their registers)
@@ -227,7 +240,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ks128_kernel(ConvK k, int tile
         });
         // the partials of every wave are in the exchange area; the next tile's halo pieces and this tile's residual
         // loads (issued a batch or more earlier) are drained first, so no LDS-DMA is in flight at any barrier
-        dma_barrier();
+        if constexpr ((DBSR_KS_ABL & 4) == 0) dma_barrier();
         // ---- epilogue of rows own0 .. own0 + HALF - 1: + partner partials, bias, act, residual, act, 16-B stores ----
         const int partner = wave ^ 4;
         const float4 b0 = *(const float4*)(lbias + 32 * q + 8 * g), b1 = *(const float4*)(lbias + 32 * q + 8 * g + 4);
@@ -242,8 +255,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ks128_kernel(ConvK k, int tile
         }
 #pragma unroll
         for (int j = 0; j < HALF; ++j) {
-            const f32x4_t o0 = __builtin_bit_cast(f32x4_t, xch[((partner * HALF + j) * 2 + 0) * 64 + ln]);
-            const f32x4_t o1 = __builtin_bit_cast(f32x4_t, xch[((partner * HALF + j) * 2 + 1) * 64 + ln]);
+            f32x4_t o0 = {0.f, 0.f, 0.f, 0.f}, o1 = o0;
+            if constexpr ((DBSR_KS_ABL & 4) == 0) {
+                o0 = __builtin_bit_cast(f32x4_t, xch[((partner * HALF + j) * 2 + 0) * 64 + ln]);
+                o1 = __builtin_bit_cast(f32x4_t, xch[((partner * HALF + j) * 2 + 1) * 64 + ln]);
+            }
             float v[8];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {

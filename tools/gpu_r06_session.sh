@@ -10,7 +10,7 @@ mode=${2:-full}
 out=gpurun_out/$tag
 mkdir -p $out
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests/test_gpu_warp_proj.py tests/test_gpu_e2e.py tests/test_gpu_resblock.py tests/test_gpu_fuse.py tests/test_gpu_weight_round.py \
+timeout -k 10 400 python -u -m pytest tests/test_gpu_ks128.py tests/test_gpu_e2e.py tests/test_gpu_resblock.py tests/test_gpu_fuse.py tests/test_gpu_weight_round.py \
     tests/test_gpu_ops.py -x -v --timeout 200 --timeout-method thread > $out/pytest_new.log 2>&1 \
     || { echo "new tests failed rc=$?"; grep -E "FAIL|Error|assert" $out/pytest_new.log | head; tail -3 $out/pytest_new.log; exit 1; }
 tail -1 $out/pytest_new.log
@@ -25,7 +25,7 @@ grep "^\[family\]" $out/bench.err | head -18
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/prof/trace -o run --output-format csv -- python3 bench.py --steps 10 \
     --warmup 3 --no-cpu-baseline --no-op-timing > $out/prof.log 2>&1 || { echo "rocprof failed"; tail -5 $out/prof.log; exit 1; }
 if [ "$mode" = full ]; then
-    re="warp512|warp_kernel|fuse_softmax|fuse512|conv3x3|conv1x1|upsample_shuffle|upsample_blur|resblock|conv_fuse|conv2d_kernel|pwc_dense|pwc_extract"
+    re="ks128|warp512|warp_kernel|fuse_softmax|fuse512|conv3x3|conv1x1|upsample_shuffle|upsample_blur|resblock|conv_fuse|conv2d_kernel|pwc_dense|pwc_extract"
     timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$re" -d $out/prof/pmc_fetch -o run --output-format csv \
         -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-op-timing > $out/pmc_fetch.log 2>&1 || { echo "pmc fetch failed"; tail -5 $out/pmc_fetch.log; exit 1; }
     timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$re" -d $out/prof/pmc_write -o run --output-format csv \
