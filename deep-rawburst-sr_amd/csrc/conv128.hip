@@ -43,7 +43,11 @@ constexpr int PER = (PIECES + NW - 1) / NW;                   // DMA pieces per 
 #ifndef DBSR_KS_ABL                                           // timing-only ablations: 1 no k-steps, 2 no halo DMA
 #define DBSR_KS_ABL 0                                         // after the first tile, 4 no partial-sum exchange
 #endif
+#ifndef DBSR_KS_RING
+#define DBSR_KS_RING 3
+#endif
 constexpr int NB = DBSR_KS_NB;                                // 16-pixel groups per MFMA batch
+constexpr int RING = DBSR_KS_RING;                            // B-fragment ring depth: reads RING - 1 k-steps ahead
 constexpr int HALF = TH / 2;                                  // groups a wave finishes (4)
 constexpr int XCH_U4 = NW * HALF * 2 * 64;                    // exchange: [wave][group][16-cout block][lane]
 constexpr int LDS_U4 = 2 * BUF_U4 + XCH_U4;
@@ -144,7 +148,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ks128_kernel(ConvK k, int tile
         unsigned ba[8];                 // byte address of pixel col + rho, k-group g (halo_phys), rho = imm & 7
 #pragma unroll
         for (int rho = 0; rho < 8; ++rho) ba[rho] = base + 16u * (4 * col + halo_phys(col + rho, g));
-        Frag<T> bq[NB][3];
+        Frag<T> bq[NB][RING];
+        constexpr int AH = RING - 1;
         auto rd = [&](auto j_, auto st_) {
             constexpr int j = decltype(j_)::value, st = decltype(st_)::value;
             constexpr int c = st / 9, tap = st % 9, imm = (J0 + j + tap / 3) * HW + tap % 3;
@@ -152,23 +157,25 @@ __global__ __launch_bounds__(512, 1) void conv3x3_ks128_kernel(ConvK k, int tile
             const unsigned a = ba[imm & 7];
             bf16x8_t v;
             asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(a), "i"(16 * (c * CH_U4 + 4 * imm)));
-            bq[j][st % 3].v = v;
+            bq[j][st % RING].v = v;
         };
-        StaticFor<0, NB>::run([&](auto j_) { rd(j_, std::integral_constant<int, 0>{}); });
-        StaticFor<0, NB>::run([&](auto j_) { rd(j_, std::integral_constant<int, 1>{}); });
+        StaticFor<0, AH>::run([&](auto s0_) {
+            StaticFor<0, NB>::run([&](auto j_) { rd(j_, s0_); });
+        });
         StaticFor<0, NS>::run([&](auto s_) {
             constexpr int st = decltype(s_)::value, c = st / 9, tap = st % 9;
             const f32x4_t z = {0.f, 0.f, 0.f, 0.f};
             StaticFor<0, NB>::run([&](auto j_) {
                 constexpr int j = decltype(j_)::value;
-                // reads issued after R(st, j): R(st, j' > j), R(st + 1, all), R(st + 2, j' < j)
-                constexpr int newer = (NB - 1 - j) + (st + 1 < NS ? NB : 0) + (st + 2 < NS ? j : 0);
-                bf16x8_t v = bq[j][st % 3].v;
+                // reads issued after R(st, j): R(st, j' > j), R(st + 1 .. st + AH - 1, all), R(st + AH, j' < j)
+                constexpr int mid = (AH - 1 < NS - 1 - st) ? AH - 1 : NS - 1 - st;
+                constexpr int newer = (NB - 1 - j) + NB * mid + (st + AH < NS ? j : 0);
+                bf16x8_t v = bq[j][st % RING].v;
                 asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(v) : "i"(newer));
-                bq[j][st % 3].v = v;
-                acc[j][0] = mma(w[c][tap][0], bq[j][st % 3], st == 0 ? z : acc[j][0]);
-                acc[j][1] = mma(w[c][tap][1], bq[j][st % 3], st == 0 ? z : acc[j][1]);
-                if constexpr (st + 2 < NS) rd(j_, std::integral_constant<int, st + 2>{});
+                bq[j][st % RING].v = v;
+                acc[j][0] = mma(w[c][tap][0], bq[j][st % RING], st == 0 ? z : acc[j][0]);
+                acc[j][1] = mma(w[c][tap][1], bq[j][st % RING], st == 0 ? z : acc[j][1]);
+                if constexpr (st + AH < NS) rd(j_, std::integral_constant<int, st + AH>{});
             });
             hook(st);
         });

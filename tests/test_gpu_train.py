@@ -86,9 +86,9 @@ def test_conv_dgrad_gate_residual(ops, dtype, case):
 # (N, Cout, H, W, Cin, expected kernel): the gated (training dgrad) epilogues of the fast kernels -- weight-
 # stationary EPI 5 on 16x8 tiles (12 frames of 48x48) and 16x16 tiles (40 frames of 32x16, 96 dgrad couts: a
 # partial cout tile), the pipelined kernel's run-time epilogue (48 frames of 48x48, 128 -> 64 channels) and its
-# epilogue 5 at the 32x16 tile (64 frames of 32x32: the training step's 128x128 weight-predictor dgrads; 96 dgrad
-# couts: a partial cout tile)
-GATED = [(12, 64, 48, 48, 64, 4), (40, 64, 32, 16, 96, 4), (48, 128, 48, 48, 64, 2), (64, 128, 32, 32, 128, 2),
+# epilogue 5 at the 32x16 tile (64 frames of 32x32, 96 dgrad couts: a partial cout tile), and the K-split 128-channel
+# kernel's epilogue 5 (64 frames of 32x32, 128 -> 128: the training step's weight-predictor ResBlock dgrads)
+GATED = [(12, 64, 48, 48, 64, 4), (40, 64, 32, 16, 96, 4), (48, 128, 48, 48, 64, 2), (64, 128, 32, 32, 128, 7),
          (64, 128, 32, 32, 96, 2)]
 
 
