@@ -600,7 +600,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_tiled_kernel(ConvK k, int tile
             for (int j = 0; j < WN / 16; ++j) acc[i][j] = mma(a[i], b[j], acc[i][j]);
     };
 
-    for (int chunk = 0; chunk < nchunks; ++chunk) {
+    // split-K (launch_tiled with k.ksplit > 1: blockIdx.y = the K slice): this block's whole 32-channel chunks
+    const int ksl = (int)gridDim.y, kz = (int)blockIdx.y;
+    const int ch0 = nchunks * kz / ksl, ch1 = nchunks * (kz + 1) / ksl;
+    for (int chunk = ch0; chunk < ch1; ++chunk) {
         issue(chunk);
         dma_barrier();                   // vmcnt(0) for the LDS-DMA + barrier
         // taps software-pipelined through two fragment sets: tap t+1's ds_reads are in flight during
@@ -619,6 +622,22 @@ __global__ __launch_bounds__(256, 2) void conv3x3_tiled_kernel(ConvK k, int tile
         __syncthreads();                 // all waves done reading before the next chunk lands
     }
 
+    if (ksl > 1) {
+        // the slice's fp32 partial sums, [slice][pixel][cw], summed in slice order (then bias, act, residual, gate)
+        // by conv_splitk_finalize
+#pragma unroll
+        for (int j = 0; j < WN / 16; ++j) {
+            const int oy = y0 + row0 + j, ox = x0 + col;
+            if (oy >= k.out_h || ox >= k.out_w) continue;
+            const long long p = ((long long)f * k.out_h + oy) * k.out_w + ox;
+#pragma unroll
+            for (int i = 0; i < WM / 16; ++i) {
+                const int co = c_base + i * 16 + g * 4;
+                if (co < k.cout) *(f32x4_t*)(k.ws + ((long long)kz * k.npix + p) * k.cw + co) = acc[i][j];
+            }
+        }
+        return;
+    }
     // ---- epilogue: bias + act into an LDS [pixel][cout] tile, then whole 16-B rows per lane ----
     const bool staged = !k.y_f32 && k.y_ld % 8 == 0 && k.y_c0 % 8 == 0 && k.cout % 8 == 0 &&
                         (!k.r || (k.r_ld % 8 == 0 && k.r_c0 % 8 == 0)) && (!k.gt || (k.g_ld % 8 == 0 && k.g_c0 % 8 == 0));
@@ -751,9 +770,14 @@ int launch_tiled(const ConvK& k, int n_frames, hipStream_t s) {
         dbsr_set_error("conv2d: grid too large");
         return DBSR_E_ARG;
     }
-    hipLaunchKernelGGL((conv3x3_tiled_kernel<T, WM, WN, D>), dim3((unsigned)nb), dim3(256), 0, s, k, tiles_x, tiles_y,
-                       nct, (int)nb);
+    hipLaunchKernelGGL((conv3x3_tiled_kernel<T, WM, WN, D>), dim3((unsigned)nb, (unsigned)k.ksplit), dim3(256), 0, s, k,
+                       tiles_x, tiles_y, nct, (int)nb);
     DBSR_LAUNCH_CHECK();
+    if (k.ksplit > 1) {
+        const long long n = (long long)k.npix * (k.cw / 4);
+        hipLaunchKernelGGL((conv_splitk_finalize<T>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, k);
+        DBSR_LAUNCH_CHECK();
+    }
     return 0;
 }
 
@@ -2083,10 +2107,36 @@ void pick_tiled_tile(const dbsr_conv_desc* d, int& wm, int& wn) {     // (d: the
     wn = 16;
 }
 
+// Split-K for the LDS-tiled kernel (16-bit, dilation 1): a long-K conv (>= 8 chunks of 32 channels) whose natural
+// tile (64 couts, or 32 for cout <= 32, x 16x16 pixels) gives under 256 blocks keeps that tile and splits its chunks
+// into K slices of >= 2 chunks until there are ~512 blocks -- the decoder's first conv (decoders.py:37, 512 -> 64 on
+// 8 frames of 48x48: 72 tiles x 8 slices) and PWC-Net's last level-2 DenseNet conv (533 -> 32 on 104 16x16 frames);
+// the slices' fp32 partials go to the workspace and conv_splitk_finalize adds them in slice order.  Returns the
+// split (1: none) and sets the tile.
+int g_tiled_split_enabled = 1;
+int tiled_ksplit(const dbsr_conv_desc* d, int& wm, int& wn) {
+    if (!g_tiled_split_enabled || !is16(d->x.dtype) || d->dil != 1) return 1;
+    const int nch = cin_pad(d->cin) / 32;
+    const int wm0 = d->cout <= 32 ? 32 : 64;
+    const int nb = tiled_blocks(d, wm0, 64);
+    if (nb >= 256 || nch < 8) return 1;
+    const int sp = std::min(nch / 2, (512 + nb - 1) / nb);
+    if (sp < 2) return 1;
+    wm = wm0;
+    wn = 64;
+    return sp;
+}
+
 template <typename T, int D>
-int dispatch_tiled_d(const ConvK& k, const dbsr_conv_desc* d, const dbsr_conv_desc* sel, hipStream_t s) {
+int dispatch_tiled_d(const ConvK& k0, const dbsr_conv_desc* d, const dbsr_conv_desc* sel, hipStream_t s) {
     int wm, wn;
     pick_tiled_tile(sel, wm, wn);
+    ConvK k = k0;
+    k.ksplit = tiled_ksplit(sel, wm, wn);
+    if (k.ksplit > 1 && splitk_bytes(k, k.ksplit) > d->workspace_bytes) {
+        k.ksplit = 1;
+        pick_tiled_tile(sel, wm, wn);
+    }
     if (wm == 64) return launch_tiled<T, 64, 64, D>(k, d->n_frames, s);
     if (wn == 128) return launch_tiled<T, 32, 128, D>(k, d->n_frames, s);
     if (wn == 64) return launch_tiled<T, 32, 64, D>(k, d->n_frames, s);
@@ -2756,7 +2806,8 @@ extern "C" int dbsr_conv_dispatch_variant(const dbsr_conv_desc* d) {
     } else if (kf == 1) {
         int wm, wn;
         pick_tiled_tile(sel, wm, wn);
-        var = wm * 1000 + wn;
+        const int sp = tiled_ksplit(sel, wm, wn);
+        var = (sp > 1 ? sp * 100000 : 0) + wm * 1000 + wn;
     } else if (kf == 0) {
         const ConvK k = make_convk(sel);
         int m, n;
@@ -2775,9 +2826,16 @@ extern "C" int dbsr_conv_head_ok(const dbsr_conv_desc* d) {
 }
 
 extern "C" size_t dbsr_conv_workspace_bytes(const dbsr_conv_desc* d) {
-    if (!d || kernel_for(d) != 0 || d->precise) return 0;
+    if (!d || d->precise) return 0;
+    const int kf = kernel_for(d);
     dbsr_conv_desc v;
     const dbsr_conv_desc* sel = sel_view(d, v);
+    if (kf == 1) {
+        int wm, wn;
+        pick_tiled_tile(sel, wm, wn);
+        return splitk_bytes(make_convk(d), tiled_ksplit(sel, wm, wn));
+    }
+    if (kf != 0) return 0;
     const ConvK ksel = make_convk(sel);
     int m, n;
     pick_generic_tile(ksel, m, n);

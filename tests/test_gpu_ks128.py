@@ -108,3 +108,34 @@ def test_ks128_not_picked_off_shape():
         w = torch.randn(cout, cin, 3, 3, device=DEV) / 34.0
         ops.conv2d(x, w, None, padding=1, compute_dtype=torch.float16)
         assert ops.conv2d.last_kernel != 7, (N, cin, H, W, cout)
+
+
+# (N, Cin, H, W, Cout, expected K split): the LDS-tiled kernel's split-K (conv2d.hip tiled_ksplit) -- the decoder's
+# first conv (512 -> 64, 8 frames of 48x48), PWC-Net's last level-2 DenseNet conv (533 -> 32, 16x16 frames) and a
+# partial cout tile (96 couts) with a ragged frame
+TILED_SPLIT = [(8, 512, 48, 48, 64, 8), (104, 533, 16, 16, 32, 5), (3, 320, 20, 17, 96, 5)]
+
+
+@pytest.mark.parametrize('dt', [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize('case', TILED_SPLIT)
+def test_tiled_split_k(dt, case):
+    """Split-K LDS-tiled 3x3 (fp32 slice partials + in-order finalize) against torch fp32 on the same 16-bit
+    operands, with bias + ReLU and with the residual / post-ReLU epilogue; the dispatch variant names the split."""
+    from dbsr_amd import ops
+    N, Cin, H, W, Cout, sp = case
+    gen = torch.Generator().manual_seed(Cin + Cout + H)
+    x = torch.randn(N, Cin, H, W, generator=gen)
+    w = torch.randn(Cout, Cin, 3, 3, generator=gen) / (Cin * 9) ** 0.5
+    b = torch.randn(Cout, generator=gen) * 0.1
+    res = torch.randn(N, Cout, H, W, generator=gen)
+    xr, wr, rr = x.to(dt).float(), w.to(dt).float(), res.to(dt).float()
+    ulp = 2.0 ** (-10 if dt == torch.float16 else -7)
+    for use_res in (False, True):
+        ref = F.conv2d(xr, wr, b, padding=1)
+        ref = F.relu(ref + rr) if use_res else F.relu(ref)
+        out = ops.conv2d(x.to(DEV), w.to(DEV), b.to(DEV), padding=1, act=0 if use_res else 1,
+                         residual=res.to(DEV) if use_res else None, post_act=1 if use_res else 0,
+                         compute_dtype=dt).float().cpu()
+        assert ops.conv2d.last_kernel == 1 and ops.conv2d.last_variant // 100000 % 10 == sp, ops.conv2d.last_variant
+        np.testing.assert_allclose(out.numpy(), ref.numpy(), atol=4 * ulp, rtol=2 * ulp)
+        assert (out - ref).abs().mean() < 0.25 * ulp
