@@ -2108,16 +2108,17 @@ void pick_tiled_tile(const dbsr_conv_desc* d, int& wm, int& wn) {     // (d: the
 }
 
 // Split-K for the LDS-tiled kernel (16-bit, dilation 1): a long-K conv (>= 8 chunks of 32 channels) whose natural
-// tile (64 couts, or 32 for cout <= 32, x 16x16 pixels) gives under 256 blocks keeps that tile and splits its chunks
-// into K slices of >= 2 chunks until there are ~512 blocks -- the decoder's first conv (decoders.py:37, 512 -> 64 on
-// 8 frames of 48x48: 72 tiles x 8 slices) and PWC-Net's last level-2 DenseNet conv (533 -> 32 on 104 16x16 frames);
-// the slices' fp32 partials go to the workspace and conv_splitk_finalize adds them in slice order.  Returns the
-// split (1: none) and sets the tile.
+// tile (64 couts x 16x16 pixels) gives under 256 blocks keeps that tile and splits its chunks into K slices of >= 2
+// chunks until there are ~512 blocks -- the decoder's first conv (decoders.py:37, 512 -> 64 on
+// 8 frames of 48x48: 72 tiles x 8 slices: 55.6 -> 47.5 us in the step, r06q); the slices' fp32 partials go to the
+// workspace and conv_splitk_finalize adds them in slice order.  Only for cout >= 64: PWC-Net's last level-2
+// DenseNet conv (533 -> 32 on 104 16x16 frames) measured 36.0 -> 41.2 us split against the 16x4-pixel tiles.
+// Returns the split (1: none) and sets the tile.
 int g_tiled_split_enabled = 1;
 int tiled_ksplit(const dbsr_conv_desc* d, int& wm, int& wn) {
-    if (!g_tiled_split_enabled || !is16(d->x.dtype) || d->dil != 1) return 1;
+    if (!g_tiled_split_enabled || !is16(d->x.dtype) || d->dil != 1 || d->cout < 64) return 1;
     const int nch = cin_pad(d->cin) / 32;
-    const int wm0 = d->cout <= 32 ? 32 : 64;
+    const int wm0 = 64;
     const int nb = tiled_blocks(d, wm0, 64);
     if (nb >= 256 || nch < 8) return 1;
     const int sp = std::min(nch / 2, (512 + nb - 1) / nb);
