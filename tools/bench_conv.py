@@ -14,6 +14,7 @@ SHAPES = [  # name, frames, H, W, cin, cout, k
     ('wp.init 192->128', 112, 48, 48, 192, 128, 3),
     ('wp.res 128->128', 112, 48, 48, 128, 128, 3),
     ('wp.res 128->128 (104 frames)', 104, 48, 48, 128, 128, 3),
+    ('wp.c1 128->128 (104 frames)', 104, 48, 48, 128, 128, 3),
     ('wp.out 128->512', 112, 48, 48, 128, 512, 3),
     ('dec.post 32->32', 8, 384, 384, 32, 32, 3),
     ('dec.pre 64->64', 8, 48, 48, 64, 64, 3),
