@@ -427,8 +427,9 @@ __device__ __forceinline__ void convt_px(const PrepArgs& a, const dbsr_tensor& i
 
 // Specialised per level (H x H pixels, C channels; PREV: a previous level exists) so every loop bound and
 // index is a compile-time constant.
-template <typename T, int H, int C, bool PREV>
-__global__ __launch_bounds__(256) void pwc_level_prep_kernel(PrepArgs a) {
+template <typename T, int H, int C, bool PREV, int NT>
+__global__ __launch_bounds__(NT) void pwc_level_prep_kernel(PrepArgs a) {
+    constexpr int NWV = NT / 64;                       // waves per block
     constexpr int W = H, NPIX = H * W, CP = cpad_c(C), C8 = CP / 8, BW = W + 8, BH = H + 8;
     __shared__ __attribute__((aligned(16))) unsigned char smem[PREP_LDS_BYTES];
     static_assert(NPIX * 16 + NPIX * CP * 2 + BH * BW * CP * 2 <= PREP_LDS_BYTES, "level tile exceeds the LDS");
@@ -449,7 +450,7 @@ __global__ __launch_bounds__(256) void pwc_level_prep_kernel(PrepArgs a) {
         float* part = (float*)(smem + NPIX * 16);     // [PNP][32] (before the first-feature image exists)
         const int nks = a.pcin32 / 32;
         const T* pd = img_ptr<T>(a.pD, pair);
-        for (int item = wave; item < 2 * NTN; item += 4) {
+        for (int item = wave; item < 2 * NTN; item += NWV) {
             const int mt = item & 1, nt = item >> 1;
             const int q = nt * 16 + col;
             const T* brow = pd + (long long)(q < PNP ? q : 0) * a.pD.ld + kgl * 8;
@@ -473,7 +474,7 @@ __global__ __launch_bounds__(256) void pwc_level_prep_kernel(PrepArgs a) {
             }
         }
         __syncthreads();
-        for (int q = t; q < NPIX; q += 256) {
+        for (int q = t; q < NPIX; q += NT) {
             const int oy = q / W, ox = q % W;
             float af[2];
             convt_px<float>(a, a.pflow, pair, 8, a.wflow, oy, ox, 0, 1, af);
@@ -502,11 +503,11 @@ __global__ __launch_bounds__(256) void pwc_level_prep_kernel(PrepArgs a) {
     // ---- first features into the LDS; the warped image's border to zero ----
     {
         const T* f1 = img_ptr<T>(a.first, pair);
-        for (int i = t; i < NPIX * C8; i += 256) {
+        for (int i = t; i < NPIX * C8; i += NT) {
             const int q = i / C8, c = i % C8;
             *(u32x4_t*)(fst + q * CP + c * 8) = *(const u32x4_t*)(f1 + (long long)q * a.first.ld + c * 8);
         }
-        for (int i = t; i < BH * BW * C8; i += 256) {
+        for (int i = t; i < BH * BW * C8; i += NT) {
             const int q = i / C8, c = i % C8;
             const int y = q / BW - 4, x = q % BW - 4;
             if ((unsigned)y >= (unsigned)H || (unsigned)x >= (unsigned)W)
@@ -517,7 +518,7 @@ __global__ __launch_bounds__(256) void pwc_level_prep_kernel(PrepArgs a) {
     // ---- backwarp of the second features (backwarp_kernel's arithmetic) into the bordered image ----
     {
         const T* sb = img_ptr<T>(a.second, pair);
-        for (int i = t; i < NPIX * C8; i += 256) {
+        for (int i = t; i < NPIX * C8; i += NT) {
             const int q = i / C8, g = i % C8;
             const int y = q / W, x = q % W;
             float v[8];
@@ -566,7 +567,7 @@ __global__ __launch_bounds__(256) void pwc_level_prep_kernel(PrepArgs a) {
         // out[y][x][(dy+4)*9 + dx+4] = G[x][x+dx] / C.  H = 16: windows x' in [-4, 12) for x < 8 and [4, 20)
         // for x >= 8; H = 8: one window [-4, 12), accumulator rows x >= 8 unused.
         constexpr int NWIN = H == 16 ? 2 : 1, NKS = CP / 32;
-        for (int job = wave; job < H * 9 * NWIN; job += 4) {
+        for (int job = wave; job < H * 9 * NWIN; job += NWV) {
             const int win = job % NWIN, dyi = (job / NWIN) % 9, y = job / (NWIN * 9);
             const int x0 = win * 8 - 4;                    // first window column
             const int ya = y + dyi - 4;                    // second-feature row (-4..H+3)
@@ -590,8 +591,8 @@ __global__ __launch_bounds__(256) void pwc_level_prep_kernel(PrepArgs a) {
             }
         }
     } else {
-        constexpr int NS = 256 / NPIX > 81 ? 81 : 256 / NPIX;
-        for (int i = t; i < NPIX * NS; i += 256) {
+        constexpr int NS = NT / NPIX > 81 ? 81 : NT / NPIX;
+        for (int i = t; i < NPIX * NS; i += NT) {
             const int q = i % NPIX, sl = i / NPIX;
             const int y = q / W, x = q % W;
             const T* fa = fst + q * CP;
@@ -617,7 +618,7 @@ __global__ __launch_bounds__(256) void pwc_level_prep_kernel(PrepArgs a) {
     // ---- assembly of [first | upflow | upfeat] ----
     if constexpr (PREV) {
         constexpr int NC = C + 4;
-        for (int i = t; i < NPIX * NC; i += 256) {
+        for (int i = t; i < NPIX * NC; i += NT) {
             const int q = i / NC, c = i % NC;
             const float v = c < C ? elem<T>::ld(fst + q * CP + c) : up[q * 4 + (c - C)];
             elem<T>::st(dst + (long long)q * a.D.ld + 81 + c, v);
@@ -625,6 +626,12 @@ __global__ __launch_bounds__(256) void pwc_level_prep_kernel(PrepArgs a) {
     }
 }
 
+// threads per block at the 16x16 level (level 2: one block per pair is the whole level's parallelism, 104 blocks
+// for the bench's 104 pairs on the side lane's CUs, so the block takes 16 waves; level 3 (8x8) 8 waves, the
+// coarser levels 4)
+#ifndef DBSR_PREP_NT16
+#define DBSR_PREP_NT16 1024
+#endif
 // the level shapes with a specialised kernel: (H, C, previous level) of the 64x64 pyramid (levels 6..2)
 #define DBSR_PREP_LEVELS(X) X(1, 196, false) X(2, 128, true) X(4, 96, true) X(8, 64, true) X(16, 32, true)
 
@@ -679,10 +686,11 @@ extern "C" int dbsr_pwc_level_prep(int P, int h, int w, int c, float scale, dbsr
     if (!launched && h == HH && c == CC) {                                                                     \
         DBSR_CHECK_ARG(has_prev == PP, "pwc_level_prep: level %dx%d x %d %s a previous level", h, w, c,          \
                        PP ? "needs" : "takes no");                                                            \
+        constexpr int NT = HH >= 16 ? DBSR_PREP_NT16 : HH == 8 ? 512 : 256;                                   \
         if (first.dtype == DBSR_BF16)                                                                          \
-            hipLaunchKernelGGL((pwc_level_prep_kernel<bf16_t, HH, CC, PP>), dim3(P), dim3(256), 0, s, a);      \
+            hipLaunchKernelGGL((pwc_level_prep_kernel<bf16_t, HH, CC, PP, NT>), dim3(P), dim3(NT), 0, s, a);   \
         else                                                                                                   \
-            hipLaunchKernelGGL((pwc_level_prep_kernel<f16_t, HH, CC, PP>), dim3(P), dim3(256), 0, s, a);       \
+            hipLaunchKernelGGL((pwc_level_prep_kernel<f16_t, HH, CC, PP, NT>), dim3(P), dim3(NT), 0, s, a);    \
         launched = true;                                                                                       \
     }
     DBSR_PREP_LEVELS(DBSR_PREP_LAUNCH)
