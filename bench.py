@@ -35,7 +35,7 @@ PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 PEAK_MFMA_TFLOPS = {'bf16': 2500.0, 'fp16': 2500.0, 'fp32': 157.3}   # dense peaks (MI355X_MICROARCH.md chip table)
 DTYPES = {'bf16': 'bfloat16', 'fp16': 'float16', 'fp32': 'float32'}
 # conv-like kernel families (MFMA-bound; bench reports each against the dense peak)
-CONV_FAMILIES = ('conv3x3_ws', 'conv3x3_ks128', 'conv3x3_pipe', 'conv3x3_tiled', 'conv3x3_narrow', 'conv2d_generic', 'conv1x1',
+CONV_FAMILIES = ('conv3x3_ws', 'conv3x3_ks128', 'conv3x3_pipe', 'conv3x3_tiled', 'conv3x3_narrow', 'conv3x3_small', 'conv2d_generic', 'conv1x1',
                  'conv1x1_shuffle', 'conv1x1_shuffle_blur', 'resblock32', 'resblock64', 'conv_fuse', 'pwc_dense',
                  'pwc_extract')
 KERNEL_DESC = {'conv3x3_ws': 'conv3x3_ws_kernel (persistent weight-stationary implicit-GEMM 3x3, Cin <= 64',
@@ -44,6 +44,8 @@ KERNEL_DESC = {'conv3x3_ws': 'conv3x3_ws_kernel (persistent weight-stationary im
                'conv3x3_pipe': 'conv3x3_pipe_kernel (persistent LDS-DMA-pipelined implicit-GEMM 3x3',
                'conv3x3_tiled': 'conv3x3_tiled_kernel (LDS-tiled implicit-GEMM 3x3',
                'conv3x3_narrow': 'conv3x3_narrow_kernel (cout <= 4 over a long K: the level-2 flow head',
+               'conv3x3_small': 'conv3x3_small_kernel (3x3 of an 8-channel input, weights in registers: the encoder / '
+                                'offset-feature first convs',
                'conv2d_generic': 'conv2d_kernel (generic implicit-GEMM',
                'conv1x1': 'conv1x1_kernel (pointwise projection, LDS-resident weights',
                'conv1x1_shuffle': 'upsample_shuffle_kernel (1x1 conv + PixelShuffle',

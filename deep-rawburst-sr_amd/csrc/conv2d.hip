@@ -2055,6 +2055,87 @@ void pick_generic_tile(const ConvK& k, int& best_m, int& best_n) {
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// 3x3 conv of an 8-channel (padded) 16-bit input: the frame encoder's first conv (encoders.py:36, 4 raw channels ->
+// 64) and the offset-feature extractor's (merging.py:85, the 2 offset channels -> 64).  K = 9 taps x 8 channels = 72,
+// packed as 3 MFMA k-steps of 4 taps (the packer's rows: k = tap * 8 + channel, taps 9-11 zero).  Each wave keeps
+// the 64 x 96 weights as A-fragments in registers (48 VGPRs) and walks 16-pixel groups: per group lane (g, col)
+// loads tap 4s + g of pixel col (16 B, one input pixel's 8 channels; out-of-frame taps zero) for k-step s, then
+// 12 MFMAs (4 16-cout blocks x 3 k-steps) and bias + act, 8-B stores of 4 couts.  The generic kernel ran these
+// as general implicit GEMMs at 22-25 us each on the whole chip (r06f) for ~31 MB of output.
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void conv3x3_small_kernel(ConvK k, int groups_x, long long ngroups) {
+    const int lane = threadIdx.x & 63, g = lane >> 4, col = lane & 15;
+    const int nco = k.cout / 16;                       // 16-cout blocks (cout % 16 == 0, <= 64)
+    Frag<T> a[4][3];
+    f32x4_t bias[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        bias[b] = load_bias4(k, min(b, nco - 1) * 16 + g * 4);
+#pragma unroll
+        for (int st = 0; st < 3; ++st)
+            a[b][st].load((const T*)k.w + (long long)(min(b, nco - 1) * 16 + col) * k.Kp + 32 * st + 8 * g);
+    }
+    const long long wave0 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const long long nwaves = ((long long)gridDim.x * blockDim.x) >> 6;
+    for (long long gi = wave0; gi < ngroups; gi += nwaves) {
+        const int gx = (int)(gi % groups_x);
+        const long long r = gi / groups_x;
+        const int y = (int)(r % k.out_h), f = (int)(r / k.out_h);
+        const int x = gx * 16 + col;
+        const T* xf = (const T*)k.x + map_frame(k.xm, f) * k.x_is;
+        Frag<T> bq[3];
+#pragma unroll
+        for (int st = 0; st < 3; ++st) {
+            const int tap = 4 * st + g, ky = tap / 3, kx = tap - 3 * (tap / 3);
+            const int iy = y + ky - 1, ix = x + kx - 1;
+            if (tap < 9 && (unsigned)iy < (unsigned)k.in_h && (unsigned)ix < (unsigned)k.in_w)
+                bq[st].load(xf + ((long long)iy * k.in_w + ix) * k.x_ld);
+            else
+                bq[st].zero();
+        }
+        f32x4_t acc[4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            acc[b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int st = 0; st < 3; ++st) acc[b] = mma(a[b][st], bq[st], acc[b]);
+        }
+        if (x < k.out_w) {
+            T* yp = (T*)k.y + map_frame(k.ym, f) * k.y_is + k.y_c0 + ((long long)y * k.out_w + x) * k.y_ld + 4 * g;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                if (b >= nco) break;
+                uint2 o;
+                o.x = H16<T>::pack(apply_act(acc[b][0] + bias[b][0], k.act), apply_act(acc[b][1] + bias[b][1], k.act));
+                o.y = H16<T>::pack(apply_act(acc[b][2] + bias[b][2], k.act), apply_act(acc[b][3] + bias[b][3], k.act));
+                *(uint2*)(yp + 16 * b) = o;
+            }
+        }
+    }
+}
+
+int g_small_enabled = 1;
+// conv3x3_small_kernel serves `d`: 16-bit 3x3/s1/p1/d1, cin <= 8, cout a multiple of 16 up to 64, NHWC output of the
+// input dtype (y.ld, y.c0 multiples of 4), no residual or gate
+bool use_small(const dbsr_conv_desc* d) {
+    return g_small_enabled && is16(d->x.dtype) && !d->precise && d->kh == 3 && d->kw == 3 && d->stride == 1 &&
+           d->pad == 1 && d->dil == 1 && d->cin <= 8 && d->cout % 16 == 0 && d->cout <= 64 &&
+           d->out_mode == DBSR_OUT_NHWC && d->y.dtype == d->x.dtype && d->y.ld % 4 == 0 && d->y.c0 % 4 == 0 &&
+           !d->res.ptr && !d->gate.ptr;
+}
+template <typename T>
+int launch_small(const ConvK& k, const dbsr_conv_desc* d, hipStream_t s) {
+    const int gx = (d->out_w + 15) / 16;
+    const long long ng = (long long)d->n_frames * d->out_h * gx;
+    const long long want = (ng + 15) / 16;             // ~4 groups per wave
+    const unsigned grid = (unsigned)std::max<long long>(1, std::min<long long>(want, 4096));
+    hipLaunchKernelGGL((conv3x3_small_kernel<T>), dim3(grid), dim3(256), 0, s, k, gx, ng);
+    DBSR_LAUNCH_CHECK();
+    return 0;
+}
+
 // narrow-output 3x3 convs over a long K (conv3x3_narrow_kernel): 16-bit 3x3/s1/p1/d1, cout <= 4, cin >= 256,
 // NHWC output without gate
 int g_narrow_enabled = 1;
@@ -2164,6 +2245,7 @@ int dispatch_conv(const ConvK& k, const dbsr_conv_desc* d, const dbsr_conv_desc*
         if (cfg && !pipe_fits(cfg, d)) return slab_misfit(d, sel);
         if (cfg) return dispatch_pipe<T>(cfg, k, d, s);
         if (use_narrow(sel)) return launch_narrow<T>(k, d, s);
+        if (use_small(sel)) return launch_small<T>(k, d, s);
     }
     if (use_tiled(sel)) {
         switch (d->dil) {
@@ -2748,6 +2830,7 @@ int kernel_for(const dbsr_conv_desc* d) {
         if (use_ks128(sel)) return 7;
         if (pick_pipe(sel)) return 2;
         if (use_narrow(sel)) return 6;
+        if (use_small(sel)) return 8;
     }
     return use_tiled(sel) ? 1 : 0;
 }
@@ -2852,6 +2935,7 @@ extern "C" int dbsr_set_conv_algo(int algo) {
     g_ws_enabled = algo == 2 || algo == 5;
     g_ks128_enabled = algo == 2;
     g_narrow_enabled = algo >= 2;
+    g_small_enabled = algo >= 2;
     return 0;
 }
 

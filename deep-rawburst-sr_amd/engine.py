@@ -292,7 +292,7 @@ class Plan:
             self.kernel[len(self.ops) - 1] = 'conv3x3_pipe'
             return d
         self.add(name, L.lib().dbsr_conv2d, ctypes.byref(d), work=('flop', flop))
-        self.kernel[len(self.ops) - 1] = {4: 'conv3x3_ws', 7: 'conv3x3_ks128', 2: 'conv3x3_pipe', 1: 'conv3x3_tiled', 3: 'conv1x1_shuffle', 5: 'conv1x1', 6: 'conv3x3_narrow'}.get(L.lib().dbsr_conv_kernel_for(d),
+        self.kernel[len(self.ops) - 1] = {4: 'conv3x3_ws', 7: 'conv3x3_ks128', 2: 'conv3x3_pipe', 1: 'conv3x3_tiled', 3: 'conv1x1_shuffle', 5: 'conv1x1', 6: 'conv3x3_narrow', 8: 'conv3x3_small'}.get(L.lib().dbsr_conv_kernel_for(d),
                                                                                       'conv2d_generic')
         return d
 

@@ -133,7 +133,8 @@ int dbsr_set_conv_algo(int algo);
  * (16-bit 1x1, cin 32..512 a power of two, cout 32 | 64, no residual: merging.py:34), 4 weight-stationary,
  * 3 PixelShuffle upsampler (bf16 1x1 with DBSR_OUT_SHUFFLE, 32 channels per sub-pixel), 2 pipelined,
  * 6 narrow-output 3x3 (16-bit, cout <= 4, cin >= 256, pad 1: the PWC level-2 flow head), 7 K-split
- * weight-stationary 128 -> 128 3x3 (ABI 21), 1 LDS-tiled, 0 generic. */
+ * weight-stationary 128 -> 128 3x3 (ABI 21), 8 small-input 3x3 (16-bit, cin <= 8, cout a multiple of 16 up to 64,
+ * no residual / gate: the encoder's and offset-feature extractor's first convs, ABI 21), 1 LDS-tiled, 0 generic. */
 int dbsr_conv_kernel_for(const dbsr_conv_desc* d);
 /* The full dispatch decision for `d`: kernel_for * 1000000 + the variant (weight-stationary: tile width*100 +
  * height; pipelined: tile config; LDS-tiled: cout tile*1000 + pixel tile; generic: cout tile*10000 + pixel

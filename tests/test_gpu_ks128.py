@@ -139,3 +139,30 @@ def test_tiled_split_k(dt, case):
         assert ops.conv2d.last_kernel == 1 and ops.conv2d.last_variant % 1000000 // 100000 == sp, ops.conv2d.last_variant
         np.testing.assert_allclose(out.numpy(), ref.numpy(), atol=4 * ulp, rtol=2 * ulp)
         assert (out - ref).abs().mean() < 0.25 * ulp
+
+
+# (N, Cin, H, W, Cout): the small-input 3x3 kernel (conv2d.hip conv3x3_small_kernel, kernel_for 8) -- the encoder's
+# first conv (4 raw channels -> 64), the offset-feature extractor's (2 offset channels -> 64), a ragged frame width
+# and a 16-cout conv
+SMALL = [(14, 4, 48, 48, 64), (13, 2, 48, 48, 64), (3, 8, 20, 37, 32), (2, 3, 16, 16, 16)]
+
+
+@pytest.mark.parametrize('dt', [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize('case', SMALL)
+def test_small_input_conv(dt, case):
+    """conv3x3_small_kernel against torch fp32 on the same 16-bit operands (bias + ReLU, and no activation)."""
+    from dbsr_amd import ops
+    N, Cin, H, W, Cout = case
+    gen = torch.Generator().manual_seed(Cin * 13 + Cout + W)
+    x = torch.randn(N, Cin, H, W, generator=gen)
+    w = torch.randn(Cout, Cin, 3, 3, generator=gen) / (Cin * 9) ** 0.5
+    b = torch.randn(Cout, generator=gen) * 0.1
+    xr, wr = x.to(dt).float(), w.to(dt).float()
+    ulp = 2.0 ** (-10 if dt == torch.float16 else -7)
+    for act in (1, 0):
+        ref = F.conv2d(xr, wr, b, padding=1)
+        if act:
+            ref = F.relu(ref)
+        out = ops.conv2d(x.to(DEV), w.to(DEV), b.to(DEV), padding=1, act=act, compute_dtype=dt).float().cpu()
+        assert ops.conv2d.last_kernel == 8
+        np.testing.assert_allclose(out.numpy(), ref.numpy(), atol=4 * ulp, rtol=2 * ulp)

@@ -26,7 +26,7 @@ KERNELS = {   # label -> (name predicate, algorithmic bytes per launch at the de
 
 # kernel name -> bench.py family (bench.py CONV_FAMILIES / roofline_hbm keys)
 FAMILY = [('conv3x3_ws_kernel', 'conv3x3_ws'), ('conv3x3_ks128_kernel', 'conv3x3_ks128'), ('conv3x3_pipe_kernel', 'conv3x3_pipe'),
-          ('conv3x3_tiled_kernel', 'conv3x3_tiled'), ('conv3x3_narrow_kernel', 'conv3x3_narrow'),
+          ('conv3x3_tiled_kernel', 'conv3x3_tiled'), ('conv3x3_narrow_kernel', 'conv3x3_narrow'), ('conv3x3_small_kernel', 'conv3x3_small'),
           ('conv1x1_kernel', 'conv1x1'),
           ('upsample_shuffle_kernel', 'conv1x1_shuffle'), ('upsample_blur_kernel', 'conv1x1_shuffle_blur'),
           ('resblock32_kernel', 'resblock32'), ('resblock64_kernel', 'resblock64'), ('conv_fuse_kernel', 'conv_fuse'), ('conv2d_kernel', 'conv2d_generic'),
