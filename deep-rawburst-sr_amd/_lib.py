@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get('DBSR_HIP_LIB', os.path.join(_HERE, 'libdbsr_hip.so'))
 DBSR_F32, DBSR_BF16, DBSR_F16 = 0, 1, 2
 ACT_NONE, ACT_RELU, ACT_LRELU = 0, 1, 2
 OUT_NHWC, OUT_SHUFFLE, OUT_NCHW_F32 = 0, 1, 2
-ABI_VERSION = 21
+ABI_VERSION = 22
 
 
 class FrameMap(ctypes.Structure):
@@ -41,6 +41,14 @@ class PwcExtConv(ctypes.Structure):
     """dbsr_pwc_ext_conv (include/dbsr_hip.h)."""
     _fields_ = [('w', ctypes.c_void_p), ('bias', ctypes.c_void_p), ('cin', ctypes.c_int), ('cout', ctypes.c_int),
                 ('stride', ctypes.c_int)]
+
+
+class PackJob(ctypes.Structure):
+    """dbsr_pack_job (include/dbsr_hip.h): one conv of a batched repack."""
+    _fields_ = [('w', ctypes.c_void_p), ('bias', ctypes.c_void_p), ('w_packed', ctypes.c_void_p),
+                ('bias_out', ctypes.c_void_p), ('cout', ctypes.c_int), ('cin', ctypes.c_int), ('kh', ctypes.c_int),
+                ('kw', ctypes.c_int), ('dtype', ctypes.c_int), ('shuffle', ctypes.c_int), ('transposed', ctypes.c_int),
+                ('lo', ctypes.c_int), ('src_cin', ctypes.c_int), ('pad_', ctypes.c_int), ('blk0', ctypes.c_longlong)]
 
 
 class ConvDesc(ctypes.Structure):
@@ -79,6 +87,8 @@ def lib():
             'dbsr_weights_round_diffuse': ([c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p], c_int),
             'dbsr_conv_pack_weights': ([c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
                                         c_void_p, c_void_p], c_int),
+            'dbsr_pack_batch_prepare': ([ctypes.POINTER(PackJob), c_int], c_ll),
+            'dbsr_conv_pack_weights_batch': ([c_void_p, c_int, c_ll, c_void_p], c_int),
             'dbsr_conv2d': ([ctypes.POINTER(ConvDesc), c_void_p], c_int),
             'dbsr_set_conv_algo': ([c_int], c_int),
             'dbsr_conv_kernel_for': ([ctypes.POINTER(ConvDesc)], c_int),
@@ -175,6 +185,7 @@ def lib():
 
 
 EXPORTED = ['dbsr_abi_version', 'dbsr_last_error', 'dbsr_conv_packed_elems', 'dbsr_conv_pack_weights',
+            'dbsr_pack_batch_prepare', 'dbsr_conv_pack_weights_batch',
             'dbsr_weights_round_diffuse', 'dbsr_fuse_relu_norm', 'dbsr_burst_mean', 'dbsr_conv2d',
             'dbsr_set_conv_algo', 'dbsr_conv_kernel_for', 'dbsr_conv_dispatch_variant', 'dbsr_conv_lane_reach', 'dbsr_conv_workspace_bytes', 'dbsr_conv2d_head',
             'dbsr_conv_head_ok', 'dbsr_conv_shuffle_blur', 'dbsr_conv_shuffle_blur_ok', 'dbsr_resblock', 'dbsr_resblock_ok', 'dbsr_resblock_head',

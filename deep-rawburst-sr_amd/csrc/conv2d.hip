@@ -431,6 +431,87 @@ __global__ void pack_weights_kernel(const float* __restrict__ w, const float* __
 }
 
 // ------------------------------------------------------------------------------------------------
+// Batched repack (dbsr_conv_pack_weights_batch): one launch over every job's packed elements, block b -> the job
+// whose [blk0, next blk0) holds b.  Each element is computed from the fp32 source exactly as pack_weights_kernel
+// (the row layout) and pack_weights_pipe_kernel (the chunk-major copy, which reads the row layout's element back)
+// compute it, so the result is bitwise theirs; a transposed job reads the dgrad conv's weight straight from the
+// source conv (dgrad_weights_kernel's transpose + flip, then rows [lo, lo + cout) of it).
+// ------------------------------------------------------------------------------------------------
+struct PackGeom { int CG, KG, Kp, cout_pad; long long rows; bool pipe; };
+__host__ __device__ inline PackGeom pack_geom(const dbsr_pack_job& j) {
+    PackGeom g;
+    g.CG = (j.cin <= 16 ? (j.cin + 7) / 8 * 8 : (j.cin + 31) / 32 * 32) / 8;
+    g.KG = j.kh * j.kw * g.CG;
+    g.Kp = (g.KG + 3) / 4 * 4 * 8;
+    g.cout_pad = (j.cout + 63) / 64 * 64;
+    g.rows = (long long)g.cout_pad * g.Kp;
+    g.pipe = j.kh == 3 && j.kw == 3 && j.cin > 16 && (j.dtype == DBSR_BF16 || j.dtype == DBSR_F16);
+    return g;
+}
+
+__device__ inline float pack_row_value(const dbsr_pack_job& j, const PackGeom& g, int co, int kk, int* co_src_out) {
+    int co_src = co;
+    if (j.shuffle > 1 && co < j.cout) {
+        const int s2 = j.shuffle * j.shuffle, cps = j.cout / s2;
+        const int sub = co / cps, c = co - sub * cps;
+        co_src = c * s2 + sub;
+    }
+    *co_src_out = co_src;
+    const int kg = kk >> 3, jj = kk & 7;
+    if (co < j.cout && kg < g.KG) {
+        const int tap = kg / g.CG, c = (kg - tap * g.CG) * 8 + jj;
+        if (c < j.cin) {
+            const int ky = tap / j.kw, kx = tap - ky * j.kw;
+            if (j.transposed)       // dgrad conv: out channel o = source input channel lo + o, taps flipped
+                return j.w[(((long long)c * j.src_cin + j.lo + co_src) * j.kh + (j.kh - 1 - ky)) * j.kw +
+                           (j.kw - 1 - kx)];
+            return j.w[(((long long)co_src * j.cin + c) * j.kh + ky) * j.kw + kx];
+        }
+    }
+    return 0.f;
+}
+
+__global__ __launch_bounds__(256) void pack_weights_batch_kernel(const dbsr_pack_job* __restrict__ jobs, int n) {
+    const long long b = blockIdx.x;
+    int lo = 0, hi = n - 1;             // the last job with blk0 <= b
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (jobs[mid].blk0 <= b) lo = mid;
+        else hi = mid - 1;
+    }
+    const dbsr_pack_job j = jobs[lo];
+    const PackGeom g = pack_geom(j);
+    const long long idx = (b - j.blk0) * 256 + threadIdx.x;
+    int co, kk;
+    if (idx < g.rows) {
+        co = (int)(idx / g.Kp); kk = (int)(idx - (long long)co * g.Kp);
+    } else if (g.pipe && idx < 2 * g.rows) {
+        const long long p = idx - g.rows;
+        const int e = (int)(p & 7), col = (int)((p >> 3) & 15), gg = (int)((p >> 7) & 3);
+        long long piece = p >> 9;
+        const int tap = (int)(piece % 9); piece /= 9;
+        const int nch = g.CG / 4;
+        const int c = (int)(piece % nch);
+        const long long cb16 = piece / nch;
+        const int P = j.cout <= 32 ? 32 : 64, bpt = P / 16;
+        co = (int)((cb16 / bpt) * P + pipe_cout_perm((int)(cb16 % bpt), col));
+        kk = (tap * g.CG + c * 4 + gg) * 8 + e;
+    } else {
+        return;
+    }
+    int co_src;
+    const float v = pack_row_value(j, g, co, kk, &co_src);
+    if (j.dtype == DBSR_BF16)
+        ((bf16_t*)j.w_packed)[idx] = f2bf(v);
+    else if (j.dtype == DBSR_F16)
+        ((f16_t*)j.w_packed)[idx] = (f16_t)v;
+    else
+        ((float*)j.w_packed)[idx] = v;
+    if (idx < g.rows && j.bias_out && kk == 0 && co < j.cout)
+        j.bias_out[co] = (j.bias && !j.transposed) ? j.bias[co_src] : 0.f;
+}
+
+// ------------------------------------------------------------------------------------------------
 // LDS-tiled 3x3 / stride 1 / pad 1 convolution for Cin % 32 == 0 (the ResNet trunks: encoder,
 // weight predictor, decoder; ~2/3 of the forward's FLOPs).
 //
@@ -2969,6 +3050,41 @@ extern "C" int dbsr_conv_pack_weights(const float* w_f32, const float* bias_f32,
                            (bf16_t*)w_packed + total);
         DBSR_LAUNCH_CHECK();
     }
+    return 0;
+}
+
+extern "C" long long dbsr_pack_batch_prepare(dbsr_pack_job* jobs, int n) {
+    if (!jobs || n <= 0) { dbsr_set_error("pack_batch_prepare: no jobs"); return -1; }
+    long long blk = 0;
+    for (int i = 0; i < n; ++i) {
+        dbsr_pack_job& j = jobs[i];
+        if (!j.w || !j.w_packed || j.cout <= 0 || j.cin <= 0 || j.kh <= 0 || j.kw <= 0 ||
+            !(j.dtype == DBSR_F32 || is16(j.dtype)) || j.shuffle < 1) {
+            dbsr_set_error("pack_batch_prepare: bad job %d", i);
+            return -1;
+        }
+        if (j.shuffle > 1 && (j.transposed || j.cout % (j.shuffle * j.shuffle) || (j.cout / (j.shuffle * j.shuffle)) % 4)) {
+            dbsr_set_error("pack_batch_prepare: job %d: cout %d not divisible for shuffle %d", i, j.cout, j.shuffle);
+            return -1;
+        }
+        if (j.transposed && (j.lo < 0 || j.src_cin < j.lo + j.cout)) {
+            dbsr_set_error("pack_batch_prepare: job %d: rows [%d, %d) past the source's %d input channels", i, j.lo,
+                      j.lo + j.cout, j.src_cin);
+            return -1;
+        }
+        const PackGeom g = pack_geom(j);
+        j.blk0 = blk;
+        blk += ((g.pipe ? 2 : 1) * g.rows + 255) / 256;
+    }
+    if (blk >= (1LL << 31)) { dbsr_set_error("pack_batch_prepare: too many elements"); return -1; }
+    return blk;
+}
+
+extern "C" int dbsr_conv_pack_weights_batch(const dbsr_pack_job* jobs_dev, int n, long long n_blocks, void* stream) {
+    DBSR_CHECK_ARG(jobs_dev && n > 0 && n_blocks > 0 && n_blocks < (1LL << 31), "pack_weights_batch: bad arguments");
+    hipLaunchKernelGGL(pack_weights_batch_kernel, dim3((unsigned)n_blocks), dim3(256), 0, (hipStream_t)stream,
+                       jobs_dev, n);
+    DBSR_LAUNCH_CHECK();
     return 0;
 }
 

@@ -78,6 +78,23 @@ class TConv:
         self.extra = getattr(self, 'extra', []) + [p]
         return p
 
+    def pack_jobs(self):
+        """This conv's repacks as dbsr_pack_job entries (dbsr_conv_pack_weights_batch): the forward weights and
+        every dgrad copy, the latter straight from the module's weight (no fp32 transpose pass)."""
+        code = L.dtype_code(self.fwd.dtype)
+        w = self.mod.weight
+        f = self.fwd
+        jobs = [L.PackJob(w=w.data_ptr(), bias=f.src_b.data_ptr() if f.src_b is not None else None,
+                          w_packed=f.w.data_ptr(), bias_out=f.bias.data_ptr() if f.bias is not None else None,
+                          cout=f.cout, cin=f.cin, kh=f.kh, kw=f.kw, dtype=code, shuffle=f.shuffle)]
+        for p in [self.bwd] + getattr(self, 'extra', []):
+            # p packs rows [lo, lo + p.cout) of wt = w transposed (ci, co) and flipped
+            lo = (p.src_w.data_ptr() - self.wt.data_ptr()) // (4 * self.cout * self.k * self.k)
+            jobs.append(L.PackJob(w=w.data_ptr(), bias=None, w_packed=p.w.data_ptr(),
+                                  bias_out=p.bias.data_ptr() if p.bias is not None else None, cout=p.cout, cin=p.cin,
+                                  kh=p.kh, kw=p.kw, dtype=code, shuffle=1, transposed=1, lo=lo, src_cin=self.cin))
+        return jobs
+
     def repack_ops(self, plan):
         lib = L.lib()
         plan.add('pack.' + self.name, lib.dbsr_conv_pack_weights, *self.fwd.pack_args())
@@ -96,6 +113,10 @@ class DBSRTrainer:
     `flat_grad` holds the step's gradients in the same layout (decoder first, then merging, then
     encoder: the order the backward completes them, so the bucketed all-reduce can start early).
     """
+    # re-pack every conv's weights in one launch (dbsr_conv_pack_weights_batch, bitwise the per-conv
+    # pack / dgrad-transpose / pack launches it replaces: False runs those, for A/B and the equality test)
+    BATCH_REPACK = True
+
     def __init__(self, net, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, boundary_ignore=40, process_group=None,
                  bucket_bytes=4 << 20, optimizer=True):
         dev = next(net.parameters()).device
@@ -232,8 +253,19 @@ class DBSRTrainer:
             plan.kernel[len(plan.ops) - 1] = 'conv_wgrad'
 
         # ================= forward with saved activations =================
-        for tc in self.tconvs:
-            tc.repack_ops(plan)
+        if DBSRTrainer.BATCH_REPACK:
+            # every conv's forward and dgrad weights re-packed from the updated fp32 master in one launch
+            jobs = [j for tc in self.tconvs for j in tc.pack_jobs()]
+            arr = (L.PackJob * len(jobs))(*jobs)
+            nblk = lib.dbsr_pack_batch_prepare(arr, len(jobs))
+            if nblk < 0:
+                L.check(-1, 'dbsr_pack_batch_prepare')
+            table = torch.frombuffer(bytearray(arr), dtype=torch.uint8).to(dev)
+            plan.keep.append(table)
+            plan.add('repack.all', lib.dbsr_conv_pack_weights_batch, table.data_ptr(), len(jobs), nblk)
+        else:
+            for tc in self.tconvs:
+                tc.repack_ops(plan)
         raw = NHWC(F, H, W, 8, dt, dev)
         Hp, Wp = int(math.ceil(H / 64.0) * 64), int(math.ceil(W / 64.0) * 64)
         rgb = NHWC(F, Hp, Wp, 8, dt, dev)

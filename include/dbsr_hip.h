@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define DBSR_ABI_VERSION 21
+#define DBSR_ABI_VERSION 22
 
 enum { DBSR_F32 = 0, DBSR_BF16 = 1, DBSR_F16 = 2 };
 enum { DBSR_ACT_NONE = 0, DBSR_ACT_RELU = 1, DBSR_ACT_LRELU = 2 };      /* LeakyReLU slope 0.1 */
@@ -108,6 +108,31 @@ size_t dbsr_conv_packed_elems(int cout, int cin, int kh, int kw);
  * the output channels are permuted for the DBSR_OUT_SHUFFLE epilogue (and bias_out likewise). */
 int dbsr_conv_pack_weights(const float* w_f32, const float* bias_f32, int cout, int cin, int kh, int kw,
                            int dtype, int shuffle, void* w_packed, float* bias_out, void* stream);
+/* Batched repack (ABI 22; the training step re-packs every trainable conv after each optimizer update: one launch
+ * instead of dbsr_conv_pack_weights + dbsr_dgrad_weights + dbsr_conv_pack_weights per conv, ~260 launches at the
+ * configs[3] shape).  A job packs one conv exactly as dbsr_conv_pack_weights(w, bias, cout, cin, kh, kw, dtype,
+ * shuffle, w_packed, bias_out) would (bitwise), where for transposed = 1 the weights are the dgrad conv's taken
+ * straight from the source conv's w (torch layout [cin][src_cin][kh][kw] of that conv, i.e. its cout = this job's
+ * cin): this job's output channel o, input channel c, tap (ky, kx) is w[c][lo + o][kh-1-ky][kw-1-kx] -- what
+ * dbsr_dgrad_weights followed by packing rows [lo, lo + cout) of its result gives (training.py: TConv.sub_dgrad).
+ * blk0 is filled by dbsr_pack_batch_prepare. */
+typedef struct dbsr_pack_job {
+    const float* w;
+    const float* bias;      /* NULL: no bias (bias_out, if set, gets zeros); ignored when transposed */
+    void* w_packed;
+    float* bias_out;        /* may be NULL */
+    int cout, cin, kh, kw;  /* the packed conv's shape */
+    int dtype, shuffle;
+    int transposed, lo, src_cin;
+    int pad_;
+    long long blk0;         /* first 256-element block of this job in the launch (set by dbsr_pack_batch_prepare) */
+} dbsr_pack_job;
+/* Validates the n jobs (as dbsr_conv_pack_weights does) and fills their blk0; returns the launch's block count, or
+ * -1 on a bad job (dbsr_last_error).  The caller then copies the job array to device memory once (it stays valid
+ * while the weights' and outputs' addresses do) and launches it with dbsr_conv_pack_weights_batch, which is
+ * graph-capturable. */
+long long dbsr_pack_batch_prepare(dbsr_pack_job* jobs, int n);
+int dbsr_conv_pack_weights_batch(const dbsr_pack_job* jobs_dev, int n, long long n_blocks, void* stream);
 int dbsr_conv2d(const dbsr_conv_desc* d, void* stream);
 /* Error-diffusion rounding of conv weights to the 16-bit dtype (ABI 19; replaces the implicit round-to-nearest of
  * the fp32 -> bf16/fp16 cast of the module's weights): w_out (fp32, torch layout [cout][cin][kh][kw], not aliasing

@@ -343,6 +343,42 @@ def test_train_step_graph_replay_equals_eager(synth_sd):
     torch.testing.assert_close(res[True][1], res[False][1], rtol=1e-6, atol=1e-7)
 
 
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float32])
+def test_batched_repack_bitwise(synth_sd, dtype, monkeypatch):
+    """dbsr_conv_pack_weights_batch (one launch for every conv's forward and dgrad weights, ABI 22) packs bitwise
+    what the per-conv dbsr_conv_pack_weights / dbsr_dgrad_weights / dbsr_conv_pack_weights launches pack: every
+    packed buffer (incl. the pipe copies, the shuffled upsampler and the weight predictor's sliced dgrad copies)
+    after two steps, and the steps' losses and parameters."""
+    from dbsr_amd.burst import synthetic_bursts
+    from dbsr_amd.training import DBSRTrainer
+    burst, gt = synthetic_bursts(1, 3, 24, 32, sr_factor=8, seed=29)
+    b, g = burst.to(DEV), gt.to(DEV)
+    res = {}
+    for batched in (False, True):
+        monkeypatch.setattr(DBSRTrainer, 'BATCH_REPACK', batched)
+        net, tr = _trainer(synth_sd, dtype)
+        for tc in tr.tconvs:        # (fp32 packs leave the pipe-copy half of the buffer unwritten)
+            for p in [tc.fwd, tc.bwd] + getattr(tc, 'extra', []):
+                p.w.zero_()
+        losses = [float(tr.step(b, g)) for _ in range(2)]
+        torch.cuda.synchronize()
+        names = [o[2] for o in tr.plans[(1, 3, 24, 32)].ops]
+        assert ('repack.all' in names) == batched and (any(n.startswith('packT.') for n in names) != batched)
+        bufs = []
+        for tc in tr.tconvs:
+            for p in [tc.fwd, tc.bwd] + getattr(tc, 'extra', []):
+                bufs.append(p.w.detach().clone())
+                if p.bias is not None:
+                    bufs.append(p.bias.detach().clone())
+        res[batched] = (losses, tr.flat.detach().clone(), bufs)
+    assert res[True][0] == res[False][0]
+    assert torch.equal(res[True][1], res[False][1])
+    assert len(res[True][2]) == len(res[False][2])
+    for a, c in zip(res[True][2], res[False][2]):
+        assert torch.equal(a.view(torch.int16) if a.element_size() == 2 else a,
+                           c.view(torch.int16) if c.element_size() == 2 else c)
+
+
 def _ddp_worker(rank, world, port, sd_path, data_path, out_path):
     """One rank of a 2-process DBSRTrainer run over gloo, both ranks on cuda:0 (RCCL refuses two ranks on
     one device): two steps on this rank's burst of the global batch, then its parameters and last gradients."""
