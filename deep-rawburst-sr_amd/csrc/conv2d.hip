@@ -2757,7 +2757,22 @@ __global__ __launch_bounds__(NW * 64, CT > 2 ? 1 : (PG == 1 ? 4 : 2)) void conv1
                 else b[j][ks].zero();
             }
         }
-        constexpr int CTU = CT <= 2 ? CT : 1;             // (wide couts: one 32-cout tile at a time)
+        // the wide-cout dgrad (64 -> 512 + residual): every cout tile's residual quad issued up front (CT x 4
+        // VGPRs), so the group's 16 residual loads are in flight together instead of one per cout tile (each
+        // tile's epilogue used to wait a full memory latency for its own)
+        constexpr bool RPRE = RES && CT > 2;
+        u32x4_t rq_all[RPRE ? CT : 1][PG];
+        if constexpr (RPRE) {
+#pragma unroll
+            for (int j = 0; j < PG; ++j) {
+                const T* rb = (const T*)k.r + map_frame(k.rm, pf[j] < 0 ? 0 : pf[j]) * k.r_is +
+                              (long long)prr[j] * k.r_ld + k.r_c0 + 8 * g;
+#pragma unroll
+                for (int ct = 0; ct < CT; ++ct)
+                    rq_all[ct][j] = pf[j] >= 0 ? *(const u32x4_t*)(rb + ct * 32) : u32x4_t{0u, 0u, 0u, 0u};
+            }
+        }
+        constexpr int CTU = (CT <= 2 || RPRE) ? CT : 1;   // (wide couts: one 32-cout tile at a time)
 #pragma unroll CTU
         for (int ct = 0; ct < CT; ++ct) {
             f32x4_t acc[2][PG];
@@ -2789,8 +2804,10 @@ __global__ __launch_bounds__(NW * 64, CT > 2 ? 1 : (PG == 1 ? 4 : 2)) void conv1
 #pragma unroll
                     for (int e = 0; e < 4; ++e) v[4 * h + e] = apply_act(acc[h][j][e] + bv[h][e], k.act);
                 if constexpr (RES) {                      // (training dgrad of the projection: + residual, post-act)
-                    const u32x4_t rq = *(const u32x4_t*)((const T*)k.r + map_frame(k.rm, pf[j]) * k.r_is +
-                                                          (long long)prr[j] * k.r_ld + k.r_c0 + ct * 32 + 8 * g);
+                    u32x4_t rq;
+                    if constexpr (RPRE) rq = rq_all[ct][j];
+                    else rq = *(const u32x4_t*)((const T*)k.r + map_frame(k.rm, pf[j]) * k.r_is +
+                                                (long long)prr[j] * k.r_ld + k.r_c0 + ct * 32 + 8 * g);
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
                         v[2 * e] = apply_act(v[2 * e] + H16<T>::lo(rq[e]), k.post_act);
