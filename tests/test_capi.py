@@ -109,6 +109,39 @@ def test_packed_size(L):
     assert L.lib().dbsr_conv_packed_elems(3, 32, 1, 1) == 64 * 4 * 8
 
 
+def test_pack_batch_prepare(L):
+    """dbsr_pack_batch_prepare (host only, ABI 22): 80-byte jobs; blk0 = the running sum of each job's 256-element
+    blocks (the row layout, doubled by the pipe copy for 16-bit 3x3 convs with cin > 16); bad jobs refused."""
+    lib = L.lib()
+    assert ctypes.sizeof(L.PackJob) == 80 and L.PackJob.blk0.offset == 72
+    dummy = 256
+    shapes = [(64, 64, 3, 3, L.DBSR_BF16, 1, 0, 0, 0), (64, 4, 3, 3, L.DBSR_BF16, 1, 0, 0, 0),
+              (2048, 64, 1, 1, L.DBSR_F16, 8, 0, 0, 0), (128, 128, 3, 3, L.DBSR_F32, 1, 0, 0, 0),
+              (64, 128, 3, 3, L.DBSR_BF16, 1, 1, 128, 192)]      # rows [128, 192) of a 192 -> 128 conv's dgrad
+    jobs = (L.PackJob * len(shapes))(*[L.PackJob(w=dummy, w_packed=dummy, cout=co, cin=ci, kh=kh, kw=kw, dtype=dt,
+                                                 shuffle=sh, transposed=tr, lo=lo, src_cin=sc)
+                                       for co, ci, kh, kw, dt, sh, tr, lo, sc in shapes])
+    n = lib.dbsr_pack_batch_prepare(jobs, len(shapes))
+    blk = 0
+    for j, (co, ci, kh, kw, dt, *_rest) in zip(jobs, shapes):
+        assert j.blk0 == blk
+        rows = lib.dbsr_conv_packed_elems(co, ci, kh, kw)
+        if dt == L.DBSR_F32 and kh == 3 and ci > 16:
+            rows //= 2                  # (fp32 packs carry no pipe copy; the buffer keeps its room)
+        blk += (rows + 255) // 256
+    assert n == blk
+    bad = [L.PackJob(w=None, w_packed=dummy, cout=64, cin=64, kh=3, kw=3, dtype=L.DBSR_BF16, shuffle=1),
+           L.PackJob(w=dummy, w_packed=dummy, cout=60, cin=64, kh=1, kw=1, dtype=L.DBSR_BF16, shuffle=8),
+           L.PackJob(w=dummy, w_packed=dummy, cout=64, cin=128, kh=3, kw=3, dtype=L.DBSR_BF16, shuffle=1,
+                     transposed=1, lo=160, src_cin=192),
+           L.PackJob(w=dummy, w_packed=dummy, cout=64, cin=64, kh=3, kw=3, dtype=7, shuffle=1)]
+    for b in bad:
+        one = (L.PackJob * 1)(b)
+        assert lib.dbsr_pack_batch_prepare(one, 1) == -1
+        assert b'pack_batch_prepare' in lib.dbsr_last_error()
+    assert lib.dbsr_pack_batch_prepare(jobs, 0) == -1
+
+
 def test_conv_rejects_bad_desc(L):
     lib = L.lib()
     assert lib.dbsr_conv2d(None, None) == -1
