@@ -257,7 +257,7 @@ __global__ __launch_bounds__(K == 3 ? 576 : 256) void conv_wgrad_kernel(
 // ahead, with one barrier per tile (conv_wgrad_kernel's register staging leaves one tile of compute to hide
 // each tile's load latency, and two barriers).  LDS rows of CB channels are unpadded and the 3x3 halo rows sit
 // at a pitch of XP = 24 (CB 64) / 32 (CB 32) pixels; each row's 16-B chunks are XOR-swizzled by a key taken
-// from row bits (0, 1, 3) (CB 64) / (3, 4) (CB 32), which makes a lane's key the same for every k-step (and,
+// from row bits (0, 1, 3) (CB 64) / (4, 3) (CB 32), which makes a lane's key the same for every k-step (and,
 // for the halo, depend only on the half), so the fragment addresses are per-lane bases plus immediates, and
 // the transposed reads (16 rows x 32 B) stay at the 2-cycle minimum.  A tile's barrier is passed with the next
 // tile's DMAs in flight: they target the ring stage after this one, and the stage the DMAs issued after the
@@ -290,8 +290,13 @@ __device__ __forceinline__ void wgd_dma(const void* base, unsigned bytes, int vo
     asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(r), "s"(lds_addr)
                  : "memory", "m0");
 }
+// CB 32: a 64-B row is a quarter of the 64 banks, so the rows x + q and x + 8 + q that one 32-lane half of a
+// transposed read takes (lane groups g, g + 1) share a bank quarter: their 32-B windows must sit in opposite
+// halves of the row -- key bit 1 (the window) is row bit 3, key bit 0 row bit 4.  (Bits 4, 3 the other way round
+// put both windows in one half: a 2-way conflict on every A and B read, SQ_LDS_BANK_CONFLICT = half of
+// SQ_LDS_IDX_ACTIVE at the decoder's 32-channel wgrads, r06 PMC.)
 template <int CB> __device__ __forceinline__ int wgd_swz(int row) {
-    return CB == 64 ? ((row & 3) | (((row >> 3) & 1) << 2)) : ((row >> 3) & 3);
+    return CB == 64 ? ((row & 3) | (((row >> 3) & 1) << 2)) : ((((row >> 3) & 1) << 1) | ((row >> 4) & 1));
 }
 
 template <typename T, int K, int CB>
