@@ -256,8 +256,8 @@ __global__ __launch_bounds__(K == 3 ? 576 : 256) void conv_wgrad_kernel(
 // slots, but the dY tile and the X tile go global -> LDS by buffer_load ... lds into a 3-stage ring, two tiles
 // ahead, with one barrier per tile (conv_wgrad_kernel's register staging leaves one tile of compute to hide
 // each tile's load latency, and two barriers).  LDS rows of CB channels are unpadded and the 3x3 halo rows sit
-// at a pitch of XP = 24 (CB 64) / 32 (CB 32) pixels; each row's 16-B chunks are XOR-swizzled by a key taken
-// from row bits (0, 1, 3) (CB 64) / (4, 3) (CB 32), which makes a lane's key the same for every k-step (and,
+// at a pitch of XP = 24 pixels; each row's 16-B chunks are XOR-swizzled by a key taken
+// from row bits (0, 1, 3) (CB 64) / 3 (CB 32), which makes a lane's key the same for every k-step (and,
 // for the halo, depend only on the half), so the fragment addresses are per-lane bases plus immediates, and
 // the transposed reads (16 rows x 32 B) stay at the 2-cycle minimum.  A tile's barrier is passed with the next
 // tile's DMAs in flight: they target the ring stage after this one, and the stage the DMAs issued after the
@@ -269,7 +269,7 @@ template <int K, int CB> struct WgdCfg {
     static constexpr int NW = K == 3 ? 9 : 4;
     static constexpr int RB = CB * 2;                    // row bytes
     static constexpr int CPR = RB / 16;                  // 16-B chunks per row
-    static constexpr int XP = K == 3 ? (CB == 64 ? 24 : 32) : WG_TW;    // X row pitch (pixels)
+    static constexpr int XP = K == 3 ? 24 : WG_TW;      // X row pitch (pixels)
     static constexpr int XROWS = K == 3 ? WG_HH * XP : WG_PX;          // X rows in the LDS
     static constexpr int DY_PIECES = WG_PX * CPR / 64;   // the dY rows fill whole 1-KiB pieces
     static constexpr int PIECES = ((WG_PX + XROWS) * CPR + 63) / 64;
@@ -292,11 +292,12 @@ __device__ __forceinline__ void wgd_dma(const void* base, unsigned bytes, int vo
 }
 // CB 32: a 64-B row is a quarter of the 64 banks, so the rows x + q and x + 8 + q that one 32-lane half of a
 // transposed read takes (lane groups g, g + 1) share a bank quarter: their 32-B windows must sit in opposite
-// halves of the row -- key bit 1 (the window) is row bit 3, key bit 0 row bit 4.  (Bits 4, 3 the other way round
-// put both windows in one half: a 2-way conflict on every A and B read, SQ_LDS_BANK_CONFLICT = half of
-// SQ_LDS_IDX_ACTIVE at the decoder's 32-channel wgrads, r06 PMC.)
+// halves of the row -- key bit 1 (the window) is row bit 3, which no k-step's row step (32 for dY, 2 x 24 for X)
+// changes.  (The earlier key, row bits 4, 3, put both windows in one half: a 2-way conflict on every A and B
+// read, SQ_LDS_BANK_CONFLICT = half of SQ_LDS_IDX_ACTIVE at the decoder's 32-channel wgrads, r06 PMC; it also
+// needed an X pitch of 32 pixels, whose 84-KB ring let only one of the two blocks per CU in at a time.)
 template <int CB> __device__ __forceinline__ int wgd_swz(int row) {
-    return CB == 64 ? ((row & 3) | (((row >> 3) & 1) << 2)) : ((((row >> 3) & 1) << 1) | ((row >> 4) & 1));
+    return CB == 64 ? ((row & 3) | (((row >> 3) & 1) << 2)) : (((row >> 3) & 1) << 1);
 }
 
 template <typename T, int K, int CB>
