@@ -116,6 +116,9 @@ class DBSRTrainer:
     # re-pack every conv's weights in one launch (dbsr_conv_pack_weights_batch, bitwise the per-conv
     # pack / dgrad-transpose / pack launches it replaces: False runs those, for A/B and the equality test)
     BATCH_REPACK = True
+    # forward: the weight predictor's output conv fused with the softmax + fusion (as the inference engine's
+    # DBSREngine.FUSED_WP_OUT); False: the conv into a logits buffer + dbsr_fuse_softmax
+    FUSED_WP_OUT = True
 
     def __init__(self, net, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, boundary_ignore=40, process_group=None,
                  bucket_bytes=4 << 20, optimizer=True):
@@ -317,12 +320,19 @@ class DBSRTrainer:
         plan.conv('wp.init', self.wp_init.fwd, F, WP, 0, hw, q0, 0, L.ACT_RELU)
         wp_s = res_fwd('wp.res', self.wp_res, F, hw, q0, 0, qw)
         q_last = wp_s[-1][3] if wp_s else q0
-        LG = NHWC(F, H, W, C, dt, dev)
-        plan.conv('wp.out', self.wp_out.fwd, F, q_last, 0, hw, LG, 0, L.ACT_NONE)
         FUS = NHWC(B, H, W, C, dt, dev)
         FW = NHWC(F, H, W, C, dt, dev)
-        plan.add('fuse', lib.dbsr_fuse_softmax, B, N, H * W, C, LG.d(0), E.d(0, (1, N, 0, 1)), Wf.d(0), FUS.d(0),
-                 FW.d(0))
+        # the weight predictor's output conv + softmax + fusion in one launch (dbsr_conv_fuse_softmax, fp32 logits
+        # that never reach memory: the backward needs only the weights FW, merging.py:116-124) where the library
+        # serves the shape; else the conv into 16-bit logits + dbsr_fuse_softmax
+        LG = None
+        if not (DBSRTrainer.FUSED_WP_OUT and plan.conv_fuse('wp.out+fuse', self.wp_out.fwd, B, N, q_last, hw,
+                                                             E.d(0, (1, N, 0, 1)), Wf.d(0), FUS.d(0), FW.d(0))
+                is not None):
+            LG = NHWC(F, H, W, C, dt, dev)
+            plan.conv('wp.out', self.wp_out.fwd, F, q_last, 0, hw, LG, 0, L.ACT_NONE)
+            plan.add('fuse', lib.dbsr_fuse_softmax, B, N, H * W, C, LG.d(0), E.d(0, (1, N, 0, 1)), Wf.d(0), FUS.d(0),
+                     FW.d(0))
         gd = self.dec_init.cout
         g0 = NHWC(B, H, W, gd, dt, dev)
         plan.conv('dec.init', self.dec_init.fwd, B, FUS, 0, hw, g0, 0, L.ACT_RELU)

@@ -13,7 +13,7 @@ import dbsr_amd  # noqa: E402
 from dbsr_amd.burst import synthetic_bursts  # noqa: E402
 from dbsr_amd.training import DBSRTrainer  # noqa: E402
 
-VARIANTS = {'default': dict(), 'repack0': dict(BATCH_REPACK=False)}   # (r06l also had a wgrad side-lane flag)
+VARIANTS = {'default': dict(), 'repack0': dict(BATCH_REPACK=False), 'fuse0': dict(FUSED_WP_OUT=False)}   # (r06l also had a wgrad side-lane flag)
 dev = torch.device('cuda', 0)
 burst, gt = synthetic_bursts(8, 14, 128, 128, sr_factor=8, seed=2000)
 burst, gt = burst.to(dev), gt.to(dev)
