@@ -1635,8 +1635,11 @@ int g_ws_enabled = 1;
 // tiles (WM 32: the decoder's 384x384 post-ResBlocks), aligned NHWC output / residual
 inline bool ws_narrow(const dbsr_conv_desc* d) { return d->cout <= 32; }
 // 16x8 instead of 16x16 tiles (WM 64, 32 < cin <= 64) when the 16x16 grid would cover under half the chip:
-// the decoder's pre-ResBlocks (8 frames of 48x48: 72 tiles) are a block's weight staging plus one tile
+// the decoder's pre-ResBlocks (8 frames of 48x48: 72 tiles) are a block's weight staging plus one tile; and for
+// every gated conv (the training step's dgrads, EPI 5): the 16x16 tile's gated epilogue spills 14 VGPRs, the 16x8
+// one none (training step 55.5-55.7 against 56.0-56.4 ms on one box, profiles/r06v_ws_gate_tile_ab.txt)
 inline bool ws_short(const dbsr_conv_desc* d) {
+    if (d->gate.ptr && d->cout > 32 && d->cin > 32) return true;
     return !ws_narrow(d) && d->cin > 32 && d->out_w % 16 == 0 && d->out_h % 16 == 0 &&
            (long long)d->n_frames * (d->out_w / 16) * (d->out_h / 16) * ((d->cout + 63) / 64) < 128;
 }
