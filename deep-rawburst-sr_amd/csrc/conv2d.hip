@@ -2760,24 +2760,16 @@ __global__ __launch_bounds__(NW * 64, CT > 2 ? 1 : (PG == 1 ? 4 : 2)) void conv1
                 else b[j][ks].zero();
             }
         }
-        // the wide-cout dgrad (64 -> 512 + residual): every cout tile's residual quad issued up front (CT x 4
-        // VGPRs), so the group's 16 residual loads are in flight together instead of one per cout tile (each
-        // tile's epilogue used to wait a full memory latency for its own)
+        // the wide-cout dgrad (64 -> 512 + residual): the residual quads of RPD cout tiles issued together (RPD x 4
+        // VGPRs), instead of one per cout tile (each tile's epilogue waited a full memory latency for its own).
+        // bwd.proj.oth at configs[3]: one per tile 1006 us, RPD 16 889 (the 16-tile unroll spills 104 VGPRs), 8 831,
+        // 4 805 (79 VGPRs; profiles/r06p_pw_prefetch_ab.txt)
+#ifndef DBSR_PW_RPD
+#define DBSR_PW_RPD 4
+#endif
         constexpr bool RPRE = RES && CT > 2;
-        u32x4_t rq_all[RPRE ? CT : 1][PG];
-        if constexpr (RPRE) {
-#pragma unroll
-            for (int j = 0; j < PG; ++j) {
-                const T* rb = (const T*)k.r + map_frame(k.rm, pf[j] < 0 ? 0 : pf[j]) * k.r_is +
-                              (long long)prr[j] * k.r_ld + k.r_c0 + 8 * g;
-#pragma unroll
-                for (int ct = 0; ct < CT; ++ct)
-                    rq_all[ct][j] = pf[j] >= 0 ? *(const u32x4_t*)(rb + ct * 32) : u32x4_t{0u, 0u, 0u, 0u};
-            }
-        }
-        constexpr int CTU = (CT <= 2 || RPRE) ? CT : 1;   // (wide couts: one 32-cout tile at a time)
-#pragma unroll CTU
-        for (int ct = 0; ct < CT; ++ct) {
+        constexpr int RPD = RPRE ? (DBSR_PW_RPD < CT ? DBSR_PW_RPD : CT) : 1;
+        auto tile = [&](int ct, auto&& resq) {
             f32x4_t acc[2][PG];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
@@ -2807,10 +2799,7 @@ __global__ __launch_bounds__(NW * 64, CT > 2 ? 1 : (PG == 1 ? 4 : 2)) void conv1
 #pragma unroll
                     for (int e = 0; e < 4; ++e) v[4 * h + e] = apply_act(acc[h][j][e] + bv[h][e], k.act);
                 if constexpr (RES) {                      // (training dgrad of the projection: + residual, post-act)
-                    u32x4_t rq;
-                    if constexpr (RPRE) rq = rq_all[ct][j];
-                    else rq = *(const u32x4_t*)((const T*)k.r + map_frame(k.rm, pf[j]) * k.r_is +
-                                                (long long)prr[j] * k.r_ld + k.r_c0 + ct * 32 + 8 * g);
+                    const u32x4_t rq = resq(j);
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
                         v[2 * e] = apply_act(v[2 * e] + H16<T>::lo(rq[e]), k.post_act);
@@ -2823,6 +2812,30 @@ __global__ __launch_bounds__(NW * 64, CT > 2 ? 1 : (PG == 1 ? 4 : 2)) void conv1
                 *(u32x4_t*)((T*)k.y + map_frame(k.ym, pf[j]) * k.y_is + (long long)prr[j] * k.y_ld + k.y_c0 + ct * 32 +
                             8 * g) = o;
             }
+        };
+        if constexpr (RPRE) {
+#pragma unroll 1
+            for (int c0 = 0; c0 < CT; c0 += RPD) {
+                u32x4_t rqc[RPD][PG];
+#pragma unroll
+                for (int j = 0; j < PG; ++j) {
+                    const T* rb = (const T*)k.r + map_frame(k.rm, pf[j] < 0 ? 0 : pf[j]) * k.r_is +
+                                  (long long)prr[j] * k.r_ld + k.r_c0 + 8 * g;
+#pragma unroll
+                    for (int i = 0; i < RPD; ++i)
+                        rqc[i][j] = pf[j] >= 0 ? *(const u32x4_t*)(rb + (c0 + i) * 32) : u32x4_t{0u, 0u, 0u, 0u};
+                }
+#pragma unroll
+                for (int i = 0; i < RPD; ++i) tile(c0 + i, [&](int j) { return rqc[i][j]; });
+            }
+        } else {
+            constexpr int CTU = CT <= 2 ? CT : 1;        // (wide couts: one 32-cout tile at a time)
+#pragma unroll CTU
+            for (int ct = 0; ct < CT; ++ct)
+                tile(ct, [&](int j) {
+                    return *(const u32x4_t*)((const T*)k.r + map_frame(k.rm, pf[j]) * k.r_is + (long long)prr[j] * k.r_ld +
+                                             k.r_c0 + ct * 32 + 8 * g);
+                });
         }
     }
 }
