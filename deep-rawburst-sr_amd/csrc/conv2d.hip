@@ -941,13 +941,15 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pipe_kernel(ConvK k, int tiles
     // then ReLU (ResBlock conv2), 3 plain, 4 as 2 followed by a 1x1 head (<= 4 outputs) + ReLU whose fp32
     // NCHW result is the only thing stored (the decoder's last ResBlock + RGB predictor, decoders.py:59-61);
     // 0 reads act / residual / post_act at run time; 5 is 0 for the training dgrad's gate at the 32x16 tile,
-    // whose gate is loaded in the epilogue itself (prefetched like the residual, as 0 does, it spills there)
+    // whose gate is loaded in the epilogue itself (prefetched like the residual, as 0 does, it spills there);
+    // 6 bias + LeakyReLU (PWC-Net)
     constexpr bool HEAD = EPI == 4;
     static_assert(!HEAD || WM == 32, "the head reads all 32 channels of a pixel from one cout tile");
     const bool has_res = EPI == 2 || HEAD || ((EPI == 0 || EPI == 5) && k.r != nullptr);
     auto act1 = [&](float v) {
         if constexpr (EPI == 1) return fmaxf(v, 0.f);
         else if constexpr (EPI == 0 || EPI == 5) return apply_act(v, k.act);
+        else if constexpr (EPI == 6) return v > 0.f ? v : 0.1f * v;     // (apply_act's LeakyReLU)
         else return v;
     };
     auto act2 = [&](float v) {
@@ -1263,6 +1265,9 @@ int launch_pipe(const ConvK& k, int n_frames, hipStream_t s) {
     else if (!k.r && k.act == DBSR_ACT_RELU) epi = 1;
     else if (k.r && k.act == DBSR_ACT_NONE && k.post_act == DBSR_ACT_RELU) epi = 2;
     else if (!k.r && k.act == DBSR_ACT_NONE) epi = 3;
+    // 6: bias + LeakyReLU, PWC-Net's convs: run-time epilogue 0 spilled 48 VGPRs at the 32x16 tile, 6 none
+    // (pwc.refiner0 46 -> 38 us on the chip, profiles/r06e6_pipe_epi6_ab.txt)
+    else if (!k.r && k.act == DBSR_ACT_LRELU) epi = 6;
 #define DBSR_PIPE_LAUNCH(E)                                                                                    \
     hipLaunchKernelGGL((conv3x3_pipe_kernel<T, WM, TW, TH, E>), dim3(grid), dim3(512), 0, s, k, tiles_x, tiles_y, \
                        nct, (int)nt)
@@ -1276,6 +1281,7 @@ int launch_pipe(const ConvK& k, int n_frames, hipStream_t s) {
         case 5:
             if constexpr (TW == 32 && TH == 16) DBSR_PIPE_LAUNCH(5);
             break;
+        case 6: DBSR_PIPE_LAUNCH(6); break;
         default: DBSR_PIPE_LAUNCH(0); break;
     }
 #undef DBSR_PIPE_LAUNCH
